@@ -1,0 +1,433 @@
+"""go-raytracing_amd — MI355X-native path tracer for byvfx/go-raytracing scenes.
+
+Python binding (ctypes) over the two native libraries built in ``lib/``:
+
+* ``librtgpu.so``  — the drop-in C-ABI of ``include/rtgpu.h`` (scene graph
+  upload, GPU render, tonemap, parity probes).  This is what the Go host binds
+  through cgo.
+* ``librtscene.so`` — the C++ mirror of the reference's host-side ``rt`` API
+  (``scenes.go`` builders, ``NewBVHNode``, loaders, ``NewBucketRenderer``;
+  ``include/rtscene.h``), standing in for the Go host (no Go toolchain here).
+
+There is no CPU fallback: if the libraries are missing or no GPU is present the
+calls fail loudly.  The package directory has a hyphen, so import it with
+``load_package()`` from ``__graft_entry__`` / tests (importlib by path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+REPO_DIR = os.path.dirname(PKG_DIR)
+ASSET_DIR = os.path.join(REPO_DIR, "assets")
+
+RT_OK = 0
+STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
+          -5: "RT_ERR_NO_SCENE", -6: "RT_ERR_DEVICE"}
+
+# hittable kinds (rtgpu.h)
+RT_SPHERE, RT_QUAD, RT_TRIANGLE, RT_PLANE, RT_LIST, RT_BVH_NODE, RT_BVH_LEAF = 1, 2, 3, 4, 5, 6, 7
+RT_TRANSLATE, RT_ROTATE_X, RT_ROTATE_Y, RT_ROTATE_Z, RT_SCALE, RT_VOLUME = 8, 9, 10, 11, 12, 13
+RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC, RT_DIFFUSE_LIGHT, RT_ISOTROPIC = 1, 2, 3, 4, 5
+RT_TEX_SOLID, RT_TEX_CHECKER = 1, 2
+
+
+class RtHittable(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("material", C.c_int32), ("a", C.c_int32), ("b", C.c_int32),
+                ("bbox", C.c_double * 6), ("p", C.c_double * 16)]
+
+
+class RtMaterial(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("texture", C.c_int32), ("albedo", C.c_double * 3), ("fuzz", C.c_double),
+                ("refraction_index", C.c_double)]
+
+
+class RtTexture(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("even", C.c_int32), ("odd", C.c_int32), ("albedo", C.c_double * 3),
+                ("inv_scale", C.c_double)]
+
+
+class RtEnvironment(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb", C.POINTER(C.c_double)),
+                ("rotation", C.c_double), ("use_importance_sampling", C.c_int32)]
+
+
+class RtSceneDesc(C.Structure):
+    _fields_ = [("hittables", C.POINTER(RtHittable)), ("num_hittables", C.c_int32),
+                ("children", C.POINTER(C.c_int32)), ("num_children", C.c_int32), ("root", C.c_int32),
+                ("materials", C.POINTER(RtMaterial)), ("num_materials", C.c_int32),
+                ("textures", C.POINTER(RtTexture)), ("num_textures", C.c_int32),
+                ("lights", C.POINTER(C.c_int32)), ("num_lights", C.c_int32),
+                ("environment", C.POINTER(RtEnvironment))]
+
+
+class RtCameraDesc(C.Structure):
+    _fields_ = [("image_width", C.c_int32), ("image_height", C.c_int32), ("samples_per_pixel", C.c_int32),
+                ("max_depth", C.c_int32), ("center", C.c_double * 3), ("pixel00", C.c_double * 3),
+                ("pixel_delta_u", C.c_double * 3), ("pixel_delta_v", C.c_double * 3),
+                ("defocus_angle", C.c_double), ("defocus_disk_u", C.c_double * 3),
+                ("defocus_disk_v", C.c_double * 3), ("background", C.c_double * 3),
+                ("use_sky_gradient", C.c_int32), ("phantom_hdri", C.c_int32), ("camera_motion", C.c_int32),
+                ("free_camera", C.c_int32)]
+
+
+class RtBucket(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class RtRenderParams(C.Structure):
+    _fields_ = [("samples_per_pixel", C.c_int32), ("max_depth", C.c_int32), ("sample_offset", C.c_int32),
+                ("seed", C.c_uint32), ("buckets", C.POINTER(RtBucket)), ("num_buckets", C.c_int32),
+                ("accumulate", C.c_int32)]
+
+
+class RtStats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("samples", C.c_uint64)]
+
+
+class RtWorkCounts(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("samples", "rays", "shadow_rays", "node_visits", "sphere_tests",
+                                          "quad_tests", "tri_tests", "plane_tests", "instance_visits",
+                                          "volume_tests", "material_fetches", "env_lookups")]
+
+
+class RtSceneInfo(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("nodes", "leaves", "refs", "spheres", "quads", "triangles", "planes",
+                                         "instances", "blases", "volumes", "materials", "textures", "lights",
+                                         "stack_needed", "tlas_depth", "blas_depth")] + [("device_bytes", C.c_int64)]
+
+
+class RtsSceneOptions(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("width", C.c_int32), ("aspect", C.c_double), ("spp", C.c_int32),
+                ("max_depth", C.c_int32), ("asset_dir", C.c_char_p), ("obj_path", C.c_char_p),
+                ("lucy_rings", C.c_int32), ("lucy_cols", C.c_int32)]
+
+
+_rtgpu = None
+_rtscene = None
+
+
+def _load(name: str) -> C.CDLL:
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it first (python -c 'import __graft_entry__ as g; g.build()')")
+    return C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
+def rtgpu() -> C.CDLL:
+    """The C-ABI library (include/rtgpu.h)."""
+    global _rtgpu
+    if _rtgpu is None:
+        lib = _load("librtgpu.so")
+        P, I32, U32 = C.c_void_p, C.c_int32, C.c_uint32
+        lib.rt_abi_version.restype = C.c_int
+        lib.rt_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
+        lib.rt_ctx_destroy.argtypes = [P]
+        lib.rt_ctx_destroy.restype = None
+        lib.rt_last_error.argtypes = [P]
+        lib.rt_last_error.restype = C.c_char_p
+        lib.rt_scene_upload.argtypes = [P, C.POINTER(RtSceneDesc)]
+        lib.rt_scene_get_info.argtypes = [P, C.POINTER(RtSceneInfo)]
+        lib.rt_render.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), C.POINTER(C.c_float),
+                                  C.POINTER(RtStats)]
+        lib.rt_render_device.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), P, P]
+        lib.rt_count_work.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
+                                      C.POINTER(RtWorkCounts)]
+        lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
+        lib.rt_primary_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32), C.POINTER(I32),
+                                        C.POINTER(C.c_float)]
+        _rtgpu = lib
+    return _rtgpu
+
+
+def rtscene() -> C.CDLL:
+    """The host rt mirror (include/rtscene.h)."""
+    global _rtscene
+    if _rtscene is None:
+        rtgpu()
+        lib = _load("librtscene.so")
+        P, I32 = C.c_void_p, C.c_int32
+        lib.rts_scene_create.argtypes = [C.c_char_p, C.POINTER(RtsSceneOptions), C.POINTER(P), C.c_char_p, I32]
+        lib.rts_scene_destroy.argtypes = [P]
+        lib.rts_scene_destroy.restype = None
+        lib.rts_scene_get_desc.argtypes = [P]
+        lib.rts_scene_get_desc.restype = C.POINTER(RtSceneDesc)
+        lib.rts_scene_get_camera.argtypes = [P]
+        lib.rts_scene_get_camera.restype = C.POINTER(RtCameraDesc)
+        lib.rts_scene_world_objects.argtypes = [P, C.POINTER(I32), I32]
+        lib.rts_scene_world_objects.restype = I32
+        lib.rts_renderer_create.argtypes = [P, I32, I32, I32, C.c_uint32, C.POINTER(P), C.c_char_p, I32]
+        lib.rts_renderer_destroy.argtypes = [P]
+        lib.rts_renderer_destroy.restype = None
+        lib.rts_renderer_render_pass.argtypes = [P, I32]
+        lib.rts_renderer_render_all.argtypes = [P]
+        lib.rts_renderer_is_completed.argtypes = [P]
+        lib.rts_renderer_framebuffer.argtypes = [P]
+        lib.rts_renderer_framebuffer.restype = C.POINTER(C.c_uint8)
+        lib.rts_renderer_accum.argtypes = [P]
+        lib.rts_renderer_accum.restype = C.POINTER(C.c_float)
+        lib.rts_renderer_duration_ms.argtypes = [P]
+        lib.rts_renderer_duration_ms.restype = C.c_double
+        lib.rts_renderer_save_png.argtypes = [P, C.c_char_p]
+        lib.rts_renderer_last_error.argtypes = [P]
+        lib.rts_renderer_last_error.restype = C.c_char_p
+        lib.rts_load_hdr.argtypes = [C.c_char_p, C.POINTER(I32), C.POINTER(I32), C.POINTER(C.c_double), C.c_int64]
+        lib.rts_write_synthetic_lucy_obj.argtypes = [C.c_char_p, I32, I32]
+        lib.rts_obj_triangle_count.argtypes = [C.c_char_p]
+        lib.rts_write_png.argtypes = [C.c_char_p, C.POINTER(C.c_uint8), I32, I32]
+        _rtscene = lib
+    return _rtscene
+
+
+class RTError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _f32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _i32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+# ---------------------------------------------------------------------------
+# Scenes (scenes.go builders, via librtscene)
+# ---------------------------------------------------------------------------
+class Scene:
+    """A BASELINE scene built by the host rt mirror; world wrapped in
+    NewBVHNodeFromList like main.go:77."""
+
+    def __init__(self, name: str, *, seed: int = 0x5EED, width: int = 0, aspect: float = 0.0, spp: int = 0,
+                 max_depth: int = 0, asset_dir: Optional[str] = None, obj_path: Optional[str] = None,
+                 lucy_rings: int = 0, lucy_cols: int = 0):
+        lib = rtscene()
+        self.name = name
+        opt = RtsSceneOptions(seed, width, aspect, spp, max_depth, (asset_dir or ASSET_DIR).encode(),
+                              obj_path.encode() if obj_path else None, lucy_rings, lucy_cols)
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = lib.rts_scene_create(name.encode(), C.byref(opt), C.byref(h), err, 512)
+        if rc != RT_OK:
+            raise RTError(rc, err.value.decode())
+        self._h = h
+        self._lib = lib
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.rts_scene_destroy(self._h)
+            self._h = None
+
+    @property
+    def desc(self):
+        return self._lib.rts_scene_get_desc(self._h)
+
+    @property
+    def camera(self) -> RtCameraDesc:
+        return self._lib.rts_scene_get_camera(self._h).contents
+
+    @property
+    def width(self) -> int:
+        return self.camera.image_width
+
+    @property
+    def height(self) -> int:
+        return self.camera.image_height
+
+    def world_objects(self) -> np.ndarray:
+        n = self._lib.rts_scene_world_objects(self._h, None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        self._lib.rts_scene_world_objects(self._h, _i32p(out), n)
+        return out[:n]
+
+    def hittables(self) -> np.ndarray:
+        d = self.desc.contents
+        return np.ctypeslib.as_array(C.cast(d.hittables, C.POINTER(C.c_byte)),
+                                     shape=(d.num_hittables * C.sizeof(RtHittable),)).view(
+            np.dtype([("kind", "<i4"), ("material", "<i4"), ("a", "<i4"), ("b", "<i4"), ("bbox", "<f8", 6),
+                      ("p", "<f8", 16)])).copy()
+
+    def children(self) -> np.ndarray:
+        d = self.desc.contents
+        if d.num_children == 0:
+            return np.zeros(0, np.int32)
+        return np.ctypeslib.as_array(d.children, shape=(d.num_children,)).copy()
+
+
+def buckets_array(buckets: Sequence[Sequence[int]]):
+    arr = (RtBucket * max(len(buckets), 1))()
+    for i, b in enumerate(buckets):
+        arr[i] = RtBucket(*[int(v) for v in b])
+    return arr
+
+
+def generate_buckets(width: int, height: int, bucket_size: int = 32):
+    """rt.generateBuckets (bucket_renderer.go:77-125): centre-out order (stable)."""
+    bs = []
+    for y in range(0, height, bucket_size):
+        for x in range(0, width, bucket_size):
+            bs.append((x, y, min(bucket_size, width - x), min(bucket_size, height - y)))
+    cx, cy = width // 2, height // 2
+    bs.sort(key=lambda b: (b[0] + b[2] // 2 - cx) ** 2 + (b[1] + b[3] // 2 - cy) ** 2)
+    return bs
+
+
+def make_params(spp: int, depth: int, seed: int = 1, sample_offset: int = 0, buckets=None, accumulate: bool = False):
+    keep = None
+    if buckets is not None:
+        keep = buckets_array(buckets)
+        p = RtRenderParams(spp, depth, sample_offset, seed, C.cast(keep, C.POINTER(RtBucket)), len(buckets),
+                           1 if accumulate else 0)
+    else:
+        p = RtRenderParams(spp, depth, sample_offset, seed, None, 0, 1 if accumulate else 0)
+    p._keep = keep
+    return p
+
+
+# ---------------------------------------------------------------------------
+# GPU context (rt_ctx)
+# ---------------------------------------------------------------------------
+class Context:
+    """One device's flattened scene + render entry points (rtgpu.h)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = rtgpu()
+        h = C.c_void_p()
+        rc = self._lib.rt_ctx_create(device, C.byref(h))
+        if rc != RT_OK:
+            raise RTError(rc, f"rt_ctx_create(device={device}) failed (no GPU?)")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rt_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != RT_OK:
+            raise RTError(rc, self._lib.rt_last_error(self._h).decode())
+
+    def upload(self, scene_desc) -> None:
+        self._check(self._lib.rt_scene_upload(self._h, scene_desc))
+
+    def info(self) -> RtSceneInfo:
+        i = RtSceneInfo()
+        self._check(self._lib.rt_scene_get_info(self._h, C.byref(i)))
+        return i
+
+    def render(self, camera: RtCameraDesc, params: RtRenderParams, accum: Optional[np.ndarray] = None):
+        if accum is None:
+            accum = np.zeros((camera.image_height, camera.image_width, 3), np.float32)
+        st = RtStats()
+        self._check(self._lib.rt_render(self._h, C.byref(camera), C.byref(params), _f32p(accum), C.byref(st)))
+        return accum, st
+
+    def render_device(self, camera: RtCameraDesc, params: RtRenderParams, dev_ptr: int, stream: int = 0):
+        self._check(self._lib.rt_render_device(self._h, C.byref(camera), C.byref(params), C.c_void_p(dev_ptr),
+                                               C.c_void_p(stream)))
+
+    def count_work(self, camera: RtCameraDesc, params: RtRenderParams) -> dict:
+        w = RtWorkCounts()
+        self._check(self._lib.rt_count_work(self._h, C.byref(camera), C.byref(params), C.byref(w)))
+        return {n: int(getattr(w, n)) for n, _ in RtWorkCounts._fields_}
+
+    def tonemap(self, accum: np.ndarray, spp: int) -> np.ndarray:
+        h, w = accum.shape[:2]
+        a = np.ascontiguousarray(accum, np.float32)
+        out = np.zeros((h, w, 4), np.uint8)
+        self._check(self._lib.rt_tonemap_rgba8(self._h, _f32p(a), w, h, spp,
+                                               out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out
+
+    def primary_hits(self, camera: RtCameraDesc, seed: int, sample: int = 0):
+        n = camera.image_width * camera.image_height
+        top = np.zeros(n, np.int32)
+        prim = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        self._check(self._lib.rt_primary_hits(self._h, C.byref(camera), seed, sample, _i32p(top), _i32p(prim),
+                                              _f32p(t)))
+        return top, prim, t
+
+
+# ---------------------------------------------------------------------------
+# rt.NewBucketRenderer analogue (progressive 3-pass, RGBA8 framebuffer)
+# ---------------------------------------------------------------------------
+class BucketRenderer:
+    """NewBucketRenderer(camera, world, bucketSize, numWorkers) on the GPU
+    (bucket_renderer.go:54-74); passes as in renderPass (:170-214)."""
+
+    def __init__(self, scene: Scene, bucket_size: int = 32, num_workers: int = 0, device: int = 0, seed: int = 1):
+        self._lib = rtscene()
+        self.scene = scene
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = self._lib.rts_renderer_create(scene._h, bucket_size, num_workers, device, seed, C.byref(h), err, 512)
+        if rc != RT_OK:
+            raise RTError(rc, err.value.decode())
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.rts_renderer_destroy(self._h)
+            self._h = None
+
+    def _check(self, rc):
+        if rc != RT_OK:
+            raise RTError(rc, self._lib.rts_renderer_last_error(self._h).decode())
+
+    def render_pass(self, p: int):
+        self._check(self._lib.rts_renderer_render_pass(self._h, p))
+
+    def render_all(self):
+        self._check(self._lib.rts_renderer_render_all(self._h))
+
+    def is_completed(self) -> bool:
+        return bool(self._lib.rts_renderer_is_completed(self._h))
+
+    def framebuffer(self) -> np.ndarray:
+        w, h = self.scene.width, self.scene.height
+        p = self._lib.rts_renderer_framebuffer(self._h)
+        return np.ctypeslib.as_array(p, shape=(h, w, 4)).copy()
+
+    def accum(self) -> np.ndarray:
+        w, h = self.scene.width, self.scene.height
+        return np.ctypeslib.as_array(self._lib.rts_renderer_accum(self._h), shape=(h, w, 3)).copy()
+
+    def duration_ms(self) -> float:
+        return float(self._lib.rts_renderer_duration_ms(self._h))
+
+    def save_image(self, path: str):
+        self._check(self._lib.rts_renderer_save_png(self._h, path.encode()))
+
+
+def load_hdr(path: str):
+    lib = rtscene()
+    w = C.c_int32()
+    h = C.c_int32()
+    rc = lib.rts_load_hdr(path.encode(), C.byref(w), C.byref(h), None, 0)
+    if rc != RT_OK:
+        raise RTError(rc, path)
+    out = np.zeros((h.value, w.value, 3), np.float64)
+    rc = lib.rts_load_hdr(path.encode(), C.byref(w), C.byref(h), out.ctypes.data_as(C.POINTER(C.c_double)),
+                          out.size)
+    if rc != RT_OK:
+        raise RTError(rc, path)
+    return out
+
+
+def write_png(path: str, rgba: np.ndarray):
+    a = np.ascontiguousarray(rgba, np.uint8)
+    rc = rtscene().rts_write_png(path.encode(), a.ctypes.data_as(C.POINTER(C.c_uint8)), a.shape[1], a.shape[0])
+    if rc != RT_OK:
+        raise RTError(rc, path)

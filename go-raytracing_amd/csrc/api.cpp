@@ -1,0 +1,444 @@
+// api.cpp — implementation of the C-ABI in include/rtgpu.h.
+//
+// rt_ctx owns one device's copy of the flattened scene and the scratch
+// buffers of the render launch.  Each entry point sets its device first
+// (cgo calls can land on any OS thread).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtgpu.h"
+#include "dev_layout.h"
+#include "flatten.h"
+#include "render_launch.h"
+
+using namespace rtg;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct rt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string error;
+  bool has_scene = false;
+  DScene dscene{};
+  HostScene host;
+  std::vector<DevBuf> scene_bufs;
+  size_t scene_bytes = 0;
+  // scratch
+  DevBuf partial, tiles, counters, errflag, accum, rgba, probe;
+  int4* tiles_pinned = nullptr;     // staging for async tile uploads
+  size_t tiles_pinned_n = 0;
+  hipEvent_t tiles_ev = nullptr;
+};
+
+namespace {
+
+int set_err(rt_ctx* c, int code, const std::string& m) {
+  if (c) c->error = m;
+  return code;
+}
+
+int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
+  return set_err(c, e == hipErrorOutOfMemory ? RT_ERR_OOM : RT_ERR_HIP,
+                 std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                  \
+  do {                                                \
+    hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
+  } while (0)
+
+int ensure(rt_ctx* ctx, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return RT_OK;
+  if (b.p) { (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc");
+  b.bytes = bytes;
+  return RT_OK;
+}
+
+template <typename T>
+int upload_vec(rt_ctx* ctx, const std::vector<T>& v, const T** dst) {
+  DevBuf b;
+  size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scene)");
+  b.bytes = bytes;
+  if (!v.empty()) {
+    e = hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(b.p); return hip_fail(ctx, e, "hipMemcpy(scene)"); }
+  }
+  ctx->scene_bufs.push_back(b);
+  ctx->scene_bytes += bytes;
+  *dst = static_cast<const T*>(b.p);
+  return RT_OK;
+}
+
+void free_scene(rt_ctx* ctx) {
+  for (auto& b : ctx->scene_bufs) (void)hipFree(b.p);
+  ctx->scene_bufs.clear();
+  ctx->scene_bytes = 0;
+  ctx->has_scene = false;
+}
+
+void free_buf(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+int make_camera(rt_ctx* ctx, const rt_camera_desc* c, DCamera& o) {
+  if (!c) return set_err(ctx, RT_ERR_INVALID, "camera is NULL");
+  if (c->image_width <= 0 || c->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
+  if (c->camera_motion || c->free_camera)
+    return set_err(ctx, RT_ERR_UNSUPPORTED, "camera motion / free camera (camera.go:390-434) not supported");
+  for (int a = 0; a < 3; ++a) {
+    o.center[a] = float(c->center[a]);
+    o.pixel00[a] = float(c->pixel00[a]);
+    o.du[a] = float(c->pixel_delta_u[a]);
+    o.dv[a] = float(c->pixel_delta_v[a]);
+    o.disk_u[a] = float(c->defocus_disk_u[a]);
+    o.disk_v[a] = float(c->defocus_disk_v[a]);
+    o.background[a] = float(c->background[a]);
+  }
+  o.defocus = c->defocus_angle > 0.0 ? 1 : 0;   // camera.go:380
+  o.use_sky = c->use_sky_gradient ? 1 : 0;
+  o.phantom = c->phantom_hdri ? 1 : 0;
+  o.cam_max_depth = c->max_depth;
+  o.width = c->image_width;
+  o.height = c->image_height;
+  return RT_OK;
+}
+
+// rt.generateBuckets (bucket_renderer.go:77-125): grid buckets sorted by the
+// squared distance of their centre from the image centre (stable here).
+std::vector<rt_bucket> default_buckets(int w, int h, int bs) {
+  std::vector<rt_bucket> b;
+  for (int y = 0; y < h; y += bs)
+    for (int x = 0; x < w; x += bs) b.push_back({x, y, std::min(bs, w - x), std::min(bs, h - y)});
+  int cx = w / 2, cy = h / 2;
+  std::stable_sort(b.begin(), b.end(), [&](const rt_bucket& p, const rt_bucket& q) {
+    double dx0 = double(p.x + p.width / 2 - cx), dy0 = double(p.y + p.height / 2 - cy);
+    double dx1 = double(q.x + q.width / 2 - cx), dy1 = double(q.y + q.height / 2 - cy);
+    return dx0 * dx0 + dy0 * dy0 < dx1 * dx1 + dy1 * dy1;
+  });
+  return b;
+}
+
+// Buckets -> 16x16 work tiles (one workgroup each).
+int make_tiles(rt_ctx* ctx, const rt_render_params* p, int W, int H, std::vector<int4>& tiles) {
+  std::vector<rt_bucket> bk;
+  if (p->buckets && p->num_buckets > 0) bk.assign(p->buckets, p->buckets + p->num_buckets);
+  else if (p->buckets == nullptr) bk = default_buckets(W, H, 32);
+  for (const rt_bucket& b : bk) {
+    if (b.width <= 0 || b.height <= 0 || b.x < 0 || b.y < 0 || b.x + b.width > W || b.y + b.height > H)
+      return set_err(ctx, RT_ERR_INVALID, "bucket outside the image");
+    for (int y = b.y; y < b.y + b.height; y += 16)
+      for (int x = b.x; x < b.x + b.width; x += 16)
+        tiles.push_back(make_int4(x, y, std::min(16, b.x + b.width - x), std::min(16, b.y + b.height - y)));
+  }
+  return RT_OK;
+}
+
+// Shared render path: tiles -> render kernel -> fixed-order reduce into `out`.
+int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* p, float* d_out,
+                hipStream_t st, bool count, unsigned long long* host_counters, double* ms) {
+  if (!ctx->has_scene) return set_err(ctx, RT_ERR_NO_SCENE, "no scene uploaded");
+  if (!p) return set_err(ctx, RT_ERR_INVALID, "params is NULL");
+  if (p->samples_per_pixel <= 0 || p->max_depth < 0 || p->sample_offset < 0)
+    return set_err(ctx, RT_ERR_INVALID, "bad samples/depth/offset");
+  DCamera dc{};
+  int rc = make_camera(ctx, cam, dc);
+  if (rc) return rc;
+  std::vector<int4> tiles;
+  rc = make_tiles(ctx, p, dc.width, dc.height, tiles);
+  if (rc) return rc;
+  if (tiles.empty()) return RT_OK;
+  const int ntiles = int(tiles.size());
+  const int spp = p->samples_per_pixel;
+  // Enough workgroups to fill 256 CUs several times over; chunks of samples
+  // keep per-workgroup work bounded (tail) and results deterministic.
+  int chunks = std::max(1, std::min(spp, (16384 + ntiles - 1) / ntiles));
+  int chunk_spp = (spp + chunks - 1) / chunks;
+  chunks = (spp + chunk_spp - 1) / chunk_spp;
+  const size_t stride = size_t(ntiles) * 256 * 3;
+  if ((rc = ensure(ctx, ctx->tiles, tiles.size() * sizeof(int4)))) return rc;
+  if (!count && (rc = ensure(ctx, ctx->partial, size_t(chunks) * stride * sizeof(double)))) return rc;
+  if ((rc = ensure(ctx, ctx->counters, 16 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
+  // Stage through pinned memory; wait for the previous upload to finish reading it.
+  HIPCHK(hipEventSynchronize(ctx->tiles_ev));
+  if (ctx->tiles_pinned_n < tiles.size()) {
+    if (ctx->tiles_pinned) (void)hipHostFree(ctx->tiles_pinned);
+    ctx->tiles_pinned = nullptr;
+    ctx->tiles_pinned_n = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&ctx->tiles_pinned), tiles.size() * sizeof(int4)));
+    ctx->tiles_pinned_n = tiles.size();
+  }
+  std::memcpy(ctx->tiles_pinned, tiles.data(), tiles.size() * sizeof(int4));
+  HIPCHK(hipMemcpyAsync(ctx->tiles.p, ctx->tiles_pinned, tiles.size() * sizeof(int4), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(ctx->tiles_ev, st));
+  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), st));
+  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(unsigned long long), st));
+  RenderLaunch w{};
+  w.tiles = static_cast<const int4*>(ctx->tiles.p);
+  w.ntiles = ntiles;
+  w.chunks = chunks;
+  w.chunk_spp = chunk_spp;
+  w.spp = spp;
+  w.max_depth = p->max_depth;
+  w.sample_offset = p->sample_offset;
+  w.seed = p->seed;
+  w.accumulate = p->accumulate ? 1 : 0;
+  w.partial = static_cast<double*>(ctx->partial.p);
+  w.partial_stride = stride;
+  w.counters = static_cast<unsigned long long*>(ctx->counters.p);
+  w.err = static_cast<int*>(ctx->errflag.p);
+  const int stack = ctx->host.stack_needed <= 32 ? 32 : 64;
+  if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
+  HIPCHK(launch_render(ctx->dscene, dc, w, stack, count, st));
+  if (!count) HIPCHK(launch_reduce(w, dc.width, d_out, st));
+  if (ms) HIPCHK(hipEventRecord(ctx->ev1, st));
+  if (count || ms) {
+    HIPCHK(hipStreamSynchronize(st));
+    int flag = 0;
+    HIPCHK(hipMemcpy(&flag, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
+    if (ms) {
+      float f = 0.f;
+      HIPCHK(hipEventElapsedTime(&f, ctx->ev0, ctx->ev1));
+      *ms = f;
+    }
+    if (count)
+      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  }
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_ctx_create(int device, rt_ctx** out) {
+  if (!out) return RT_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_ERR_HIP;
+  if (device < 0 || device >= n) return RT_ERR_INVALID;
+  rt_ctx* ctx = new rt_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->tiles_ev, hipEventDisableTiming) != hipSuccess) {
+    delete ctx;
+    return RT_ERR_HIP;
+  }
+  *out = ctx;
+  return RT_OK;
+}
+
+void rt_ctx_destroy(rt_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  free_scene(ctx);
+  free_buf(ctx->partial); free_buf(ctx->tiles); free_buf(ctx->counters); free_buf(ctx->errflag);
+  free_buf(ctx->accum); free_buf(ctx->rgba); free_buf(ctx->probe);
+  if (ctx->tiles_pinned) (void)hipHostFree(ctx->tiles_pinned);
+  (void)hipEventDestroy(ctx->tiles_ev);
+  (void)hipEventDestroy(ctx->ev0);
+  (void)hipEventDestroy(ctx->ev1);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->error.c_str() : "null context"; }
+
+int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
+  if (!ctx) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  free_scene(ctx);
+  std::string err;
+  int rc = flatten_scene(scene, ctx->host, err);
+  if (rc) return set_err(ctx, rc, err);
+  HostScene& h = ctx->host;
+  DScene& d = ctx->dscene;
+  d = DScene{};
+#define UP(vec, field) if ((rc = upload_vec(ctx, h.vec, &d.field))) { free_scene(ctx); return rc; }
+  UP(nodes, nodes);
+  UP(leaves, leaves);
+  UP(refs, refs);
+  UP(ref_rank, ref_rank);
+  UP(ref_top, tlas_ref_top);
+  UP(spheres, spheres);
+  UP(sphere_hidx, sphere_hidx);
+  UP(quads, quads);
+  UP(quad_hidx, quad_hidx);
+  UP(tris, tris);
+  UP(tri_aux, tri_aux);
+  UP(tri_hidx, tri_hidx);
+  UP(planes, planes);
+  UP(plane_hidx, plane_hidx);
+  UP(instances, instances);
+  UP(blas, blas);
+  UP(volumes, volumes);
+  UP(volume_hidx, volume_hidx);
+  UP(materials, materials);
+  UP(textures, textures);
+  UP(lights, lights);
+  UP(env_texels, env.texels);
+  UP(env_pdf, env.pdf);
+  UP(env_marginal, env.marginal);
+  UP(env_conditional, env.conditional);
+#undef UP
+  d.tlas = h.tlas;
+  d.env.valid = h.env_valid;
+  d.env.width = h.env_w;
+  d.env.height = h.env_h;
+  d.env.use_is = h.env_use_is;
+  d.env.rotation = h.env_rotation;
+  d.env.total_power = h.env_total_power;
+  d.num_planes = int(h.planes.size());
+  d.num_lights = int(h.lights.size());
+  d.stack_needed = h.stack_needed;
+  ctx->has_scene = true;
+  return RT_OK;
+}
+
+int rt_scene_get_info(const rt_ctx* ctx, rt_scene_info* o) {
+  if (!ctx || !o) return RT_ERR_INVALID;
+  if (!ctx->has_scene) return RT_ERR_NO_SCENE;
+  const HostScene& h = ctx->host;
+  o->nodes = int(h.nodes.size());
+  o->leaves = int(h.leaves.size());
+  o->refs = int(h.refs.size());
+  o->spheres = int(h.spheres.size());
+  o->quads = int(h.quads.size());
+  o->triangles = int(h.tris.size());
+  o->planes = int(h.planes.size());
+  o->instances = int(h.instances.size());
+  o->blases = int(h.blas.size());
+  o->volumes = int(h.volumes.size());
+  o->materials = int(h.materials.size());
+  o->textures = int(h.textures.size());
+  o->lights = int(h.lights.size());
+  o->stack_needed = h.stack_needed;
+  o->tlas_depth = h.tlas_depth;
+  o->blas_depth = h.blas_depth;
+  o->device_bytes = int64_t(ctx->scene_bytes);
+  return RT_OK;
+}
+
+int rt_render(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, float* accum_rgb,
+              rt_stats* stats) {
+  if (!ctx || !cam || !accum_rgb) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
+  const size_t n = size_t(cam->image_width) * cam->image_height * 3;
+  int rc = ensure(ctx, ctx->accum, n * sizeof(float));
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(ctx->accum.p, accum_rgb, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  double ms = 0.0;
+  rc = render_impl(ctx, cam, params, static_cast<float*>(ctx->accum.p), ctx->stream, false, nullptr, &ms);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(accum_rgb, ctx->accum.p, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (stats) {
+    stats->kernel_ms = ms;
+    // pixels covered by the buckets x samples
+    uint64_t px = 0;
+    if (params->buckets) for (int i = 0; i < params->num_buckets; ++i) px += uint64_t(params->buckets[i].width) * params->buckets[i].height;
+    else px = uint64_t(cam->image_width) * cam->image_height;
+    stats->samples = px * uint64_t(params->samples_per_pixel);
+  }
+  return RT_OK;
+}
+
+int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, float* accum_rgb_device,
+                     void* hip_stream) {
+  if (!ctx || !cam || !accum_rgb_device) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+  return render_impl(ctx, cam, params, accum_rgb_device, st, false, nullptr, nullptr);
+}
+
+int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, rt_work_counts* out) {
+  if (!ctx || !cam || !out) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  unsigned long long c[12] = {0};
+  double ms = 0.0;
+  int rc = render_impl(ctx, cam, params, nullptr, ctx->stream, true, c, &ms);
+  if (rc) return rc;
+  out->samples = c[0];
+  out->rays = c[1];
+  out->shadow_rays = c[2];
+  out->node_visits = c[3];
+  out->sphere_tests = c[4];
+  out->quad_tests = c[5];
+  out->tri_tests = c[6];
+  out->plane_tests = c[7];
+  out->instance_visits = c[8];
+  out->volume_tests = c[9];
+  out->material_fetches = c[10];
+  out->env_lookups = c[11];
+  return RT_OK;
+}
+
+int rt_tonemap_rgba8(rt_ctx* ctx, const float* accum_rgb, int32_t width, int32_t height, int32_t spp,
+                     uint8_t* rgba_out) {
+  if (!ctx || !accum_rgb || !rgba_out || width <= 0 || height <= 0 || spp <= 0) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = size_t(width) * height;
+  int rc = ensure(ctx, ctx->accum, n * 3 * sizeof(float));
+  if (rc) return rc;
+  if ((rc = ensure(ctx, ctx->rgba, n * 4))) return rc;
+  HIPCHK(hipMemcpyAsync(ctx->accum.p, accum_rgb, n * 3 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(launch_tonemap(static_cast<const float*>(ctx->accum.p), int(n), spp, static_cast<uint8_t*>(ctx->rgba.p),
+                        ctx->stream));
+  HIPCHK(hipMemcpyAsync(rgba_out, ctx->rgba.p, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return RT_OK;
+}
+
+int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t* out_top,
+                    int32_t* out_prim, float* out_t) {
+  if (!ctx || !cam || !out_top || !out_prim || !out_t) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->has_scene) return set_err(ctx, RT_ERR_NO_SCENE, "no scene uploaded");
+  DCamera dc{};
+  int rc = make_camera(ctx, cam, dc);
+  if (rc) return rc;
+  const size_t n = size_t(dc.width) * dc.height;
+  if ((rc = ensure(ctx, ctx->probe, n * 12))) return rc;
+  if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
+  int32_t* top = static_cast<int32_t*>(ctx->probe.p);
+  int32_t* prim = top + n;
+  float* t = reinterpret_cast<float*>(prim + n);
+  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), ctx->stream));
+  HIPCHK(launch_primary(ctx->dscene, dc, seed, sample, top, prim, t, static_cast<int*>(ctx->errflag.p),
+                        ctx->host.stack_needed <= 32 ? 32 : 64, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  int flag = 0;
+  HIPCHK(hipMemcpy(&flag, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,216 @@
+// dev_layout.h — flattened fp32 scene layout in HBM, shared by the host
+// flattener (flatten.cpp) and the HIP kernels (render.hip).
+//
+// The Go object graph (rt.Hittable tree, hittable.go:15-18) is flattened into:
+//   * one BVH2 node array holding the world BVH (TLAS, main.go:77) and every
+//     distinct BLAS (mesh BVH from LoadOBJ obj_loader.go:109, Box lists
+//     primitives.go:5-37); each node stores BOTH children's boxes so one 64-B
+//     fetch tests two bboxes (bvh.go:219-239 tests one box per call);
+//   * leaf records (first, count|kind|ntests) — the Go leaf wrapper
+//     BVHNode{leaf,leaf} (bvh.go:141) becomes ntests = 2;
+//   * SoA-ish primitive arrays sized for coalesced 16-B loads: spheres 32 B,
+//     quads 80 B, triangles 36 B (v0, e1, e2) + a winner-only aux record;
+//   * instances = the Go transform-wrapper chain (transform.go) applied
+//     wrapper by wrapper, exactly as the Go Hit methods do, over a BLAS;
+//   * volumes (volume.go) over a boundary list, planes pulled out of the BVH
+//     (their universe bbox, plane.go:17, would make every node infinite).
+#pragma once
+#include <stdint.h>
+#if !defined(__HIPCC__) && !defined(__host__)
+#define __host__
+#define __device__
+#endif
+
+namespace rtg {
+
+// Stack/work item tags (upper 4 bits of a 32-bit item).
+enum : uint32_t {
+  ITEM_NODE = 0u,       // internal BVH2 node index
+  ITEM_LEAF = 1u,       // leaf record index
+  ITEM_INSTANCE = 2u,   // enter instance: index = instance id
+  ITEM_INST_END = 3u,   // leave instance: restore the world-space ray
+};
+constexpr int ITEM_SHIFT = 28;
+constexpr uint32_t ITEM_MASK = (1u << ITEM_SHIFT) - 1u;
+
+// Primitive reference kinds (leaf "kind" field and ref tags).
+enum : int {
+  PK_MIXED = 0,   // leaf entries are refs (kind<<28 | index) in `refs`
+  PK_SPHERE = 1,
+  PK_QUAD = 2,
+  PK_TRI = 3,
+  PK_INSTANCE = 4,
+  PK_VOLUME = 5,
+  PK_PLANE = 6,   // only used in hit records
+};
+constexpr int REF_SHIFT = 28;
+constexpr uint32_t REF_MASK = (1u << REF_SHIFT) - 1u;
+
+// Leaf info word: count (16 bits) | kind (4 bits) << 16 | ntests (4) << 20.
+__host__ __device__ inline int leaf_count(uint32_t info) { return int(info & 0xFFFFu); }
+__host__ __device__ inline int leaf_kind(uint32_t info) { return int((info >> 16) & 0xFu); }
+__host__ __device__ inline int leaf_ntests(uint32_t info) { return int((info >> 20) & 0xFu); }
+__host__ __device__ inline uint32_t make_leaf_info(int count, int kind, int ntests) {
+  return uint32_t(count) | (uint32_t(kind) << 16) | (uint32_t(ntests) << 20);
+}
+
+// BVH2 node, 64 B: children boxes + child items (ITEM_NODE / ITEM_LEAF tagged).
+struct alignas(16) DNode {
+  float l[6];   // left child box  xmin,xmax,ymin,ymax,zmin,zmax
+  float r[6];   // right child box
+  uint32_t litem, ritem;
+  uint32_t pad0, pad1;
+};
+
+struct alignas(8) DLeaf {
+  uint32_t first;  // index into refs (PK_MIXED) or into the kind's prim array
+  uint32_t info;
+};
+
+// BVH header (TLAS or BLAS root).
+struct alignas(16) DBvh {
+  float box[6];
+  uint32_t root_item;   // ITEM_NODE or ITEM_LEAF
+  int32_t check_box;    // 1: BVHNode.Hit tests its own bbox; 0: HittableList (no box)
+};
+
+struct alignas(16) DSphere {   // sphere.go:6-11
+  float cx, cy, cz, r;         // Center.orig, Radius
+  float vx, vy, vz;            // Center.dir (velocity, NewMovingSphere)
+  int32_t mat;
+};
+
+struct alignas(16) DQuad {     // quad.go:5-14
+  float Qx, Qy, Qz, D;
+  float nx, ny, nz; int32_t mat;
+  float ux, uy, uz, pad0;
+  float vx, vy, vz, pad1;
+  float wx, wy, wz, pad2;
+};
+
+struct DTri {                  // triangle.go: v0, edge1 = v1-v0, edge2 = v2-v0
+  float v0[3], e1[3], e2[3];
+};
+
+struct alignas(16) DTriAux {   // loaded for the winning triangle only
+  float nx, ny, nz; int32_t mat;
+};
+
+struct alignas(16) DPlane {    // plane.go:5-10
+  float px, py, pz; int32_t mat;
+  float nx, ny, nz; int32_t rank;
+};
+
+// Transform wrapper kinds in an instance chain (outermost first).
+enum : int { W_TRANSLATE = 1, W_ROT_X = 2, W_ROT_Y = 3, W_ROT_Z = 4, W_SCALE = 5 };
+constexpr int MAX_WRAP = 6;
+
+struct alignas(16) DInstance {
+  int32_t nwrap;
+  int32_t blas;              // index into blas headers
+  int32_t pad0, pad1;
+  int32_t kind[MAX_WRAP];    // outermost first
+  int32_t pad2, pad3;
+  float prm[MAX_WRAP][6];    // translate: off xyz; rot: sin, cos; scale: f xyz, invf xyz
+};
+
+struct alignas(16) DVolume {   // volume.go:9-13
+  int32_t boundary;          // instance index describing the boundary (chain + list)
+  float neg_inv_density;
+  int32_t mat;               // phase function (Isotropic)
+  int32_t vol_id;            // RNG dimension slot
+};
+
+struct alignas(16) DMaterial {
+  int32_t kind;              // rt_material_kind
+  int32_t tex;
+  float fuzz, ior;
+  float albedo[3];
+  int32_t pad;
+};
+
+struct alignas(16) DTexture {
+  int32_t kind;              // 1 solid, 2 checker (even/odd solid)
+  float inv_scale;
+  int32_t pad0, pad1;
+  float even[4];             // solid colour / checker even colour
+  float odd[4];
+};
+
+struct alignas(16) DLight {    // camera.go:610-678 (only *Quad lights contribute)
+  float Q[4];                  // Q.xyz, area
+  float u[4];                  // u.xyz, is_quad (1/0)
+  float v[4];                  // v.xyz, mat (as float bits via int below)
+  float n[4];                  // normal.xyz
+  int32_t mat, is_quad, pad0, pad1;
+};
+
+struct DEnv {
+  int32_t valid, width, height, use_is;
+  float rotation;
+  float total_power;
+  const float* texels;       // width*height*4 (rgb + pad)
+  const float* pdf;          // width*height (normalised, hdri.go:217-219)
+  const float* marginal;     // height+1
+  const float* conditional;  // height*(width+1)
+};
+
+// Everything the kernels need, passed by value as a kernel argument.
+struct DScene {
+  const DNode* nodes;
+  const DLeaf* leaves;
+  const uint32_t* refs;
+  const int32_t* ref_rank;     // DFS rank of each TLAS ref (tie rule)
+  const DSphere* spheres;
+  const DQuad* quads;
+  const DTri* tris;
+  const DTriAux* tri_aux;
+  const DPlane* planes;
+  const DInstance* instances;
+  const DBvh* blas;
+  const DVolume* volumes;
+  const DMaterial* materials;
+  const DTexture* textures;
+  const DLight* lights;
+  // hit -> hittable index maps (parity probe)
+  const int32_t* tlas_ref_top;   // per TLAS ref: top-level hittable index
+  const int32_t* sphere_hidx;
+  const int32_t* quad_hidx;
+  const int32_t* tri_hidx;
+  const int32_t* plane_hidx;
+  const int32_t* volume_hidx;
+  DBvh tlas;
+  DEnv env;
+  int32_t num_planes;
+  int32_t num_lights;
+  int32_t stack_needed;
+  int32_t pad;
+};
+
+struct DCamera {
+  float center[3];
+  float pixel00[3];
+  float du[3], dv[3];
+  float disk_u[3], disk_v[3];
+  float background[3];
+  int32_t defocus;       // DefocusAngle > 0
+  int32_t use_sky;
+  int32_t phantom;
+  int32_t cam_max_depth; // Camera.MaxDepth (camera.go:456)
+  int32_t width, height;
+};
+
+// RNG counter layout: counter = bounce<<16 | domain<<12 | index
+enum : uint32_t {
+  DOM_CAMERA = 0,   // 0,1 jitter; 2 time; 3+2k disk try k
+  DOM_SCATTER = 1,  // 3k..3k+2: RandomUnitVector try k
+  DOM_FRESNEL = 2,  // 0
+  DOM_NEE = 3,      // 0 light select; 1,2 light point; 3,4 HDRI xi1, xi2; 5.. HDRI fallback dir
+  DOM_VOL = 4,      // vol_id*4 + pass (closest-hit ray)
+  DOM_VOL_SH_AREA = 5,
+  DOM_VOL_SH_HDRI = 6,
+};
+constexpr int MAX_UNIT_TRIES = 64;
+constexpr int MAX_DISK_TRIES = 64;
+
+}  // namespace rtg

@@ -1,0 +1,573 @@
+// flatten.cpp — flattens the Go object graph handed across the C-ABI
+// (rt_scene_desc: one rt_hittable per concrete rt.Hittable) into the fp32
+// device layout of dev_layout.h.
+//
+// Structure kept from the reference (so traversal work is comparable):
+//   * the world BVH topology exactly as the caller built it (NewBVHNode,
+//     bvh.go:69-217, median split on the longest centroid axis, leaf <= 4),
+//     re-expressed as BVH2 nodes holding both children's boxes;
+//   * infinite planes are lifted out of the world BVH (plane.go:17 gives them
+//     a universe bbox) and the node boxes are refit without them;
+//   * every distinct BLAS (mesh BVH / Box list) is flattened once and shared
+//     by all instances (scenes.go:776-801 reuses one Lucy BVH 10 times);
+//   * transform wrapper chains (transform.go:24-46) become an instance chain
+//     applied wrapper by wrapper on the device.
+// Ranks: every top-level object gets its position in the reference's
+// left-first DFS order; BLAS primitives are laid out in that order too.  The
+// device tie rule (render.hip, Best/accept) uses them.
+#include "flatten.h"
+
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <map>
+#include <sstream>
+
+namespace rtg {
+
+float round_down(double x) {
+  float f = float(x);
+  if (std::isfinite(x) && double(f) > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+float round_up(double x) {
+  float f = float(x);
+  if (std::isfinite(x) && double(f) < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  return f;
+}
+
+namespace {
+
+constexpr double kInf = std::numeric_limits<double>::infinity();
+
+struct Box {
+  double b[6] = {kInf, -kInf, kInf, -kInf, kInf, -kInf};
+  bool empty() const { return !(b[0] <= b[1]); }
+  void merge(const double* o) {
+    for (int a = 0; a < 3; ++a) {
+      if (o[2 * a] < b[2 * a]) b[2 * a] = o[2 * a];
+      if (o[2 * a + 1] > b[2 * a + 1]) b[2 * a + 1] = o[2 * a + 1];
+    }
+  }
+  void merge(const Box& o) { if (!o.empty()) merge(o.b); }
+};
+
+void store_box(float* dst, const Box& bx) {
+  if (bx.empty()) {
+    for (int a = 0; a < 3; ++a) {
+      dst[2 * a] = std::numeric_limits<float>::infinity();
+      dst[2 * a + 1] = -std::numeric_limits<float>::infinity();
+    }
+    return;
+  }
+  for (int a = 0; a < 3; ++a) {
+    dst[2 * a] = round_down(bx.b[2 * a]);
+    dst[2 * a + 1] = round_up(bx.b[2 * a + 1]);
+  }
+}
+
+struct Flattener {
+  const rt_scene_desc* d;
+  HostScene& S;
+  std::string& err;
+  int status = RT_OK;
+  int rank_counter = 0;
+  std::map<int, int> blas_memo;     // graph index -> blas id
+  std::map<int, int> vol_ids;       // graph index of volume -> vol_id
+  uint32_t empty_leaf = 0;
+
+  Flattener(const rt_scene_desc* desc, HostScene& s, std::string& e) : d(desc), S(s), err(e) {}
+
+  bool fail(int code, const std::string& m) {
+    if (status == RT_OK) { status = code; err = m; }
+    return false;
+  }
+  const rt_hittable& H(int i) const { return d->hittables[i]; }
+  bool valid_index(int i) const { return i >= 0 && i < d->num_hittables; }
+  bool child_range(const rt_hittable& h) const {
+    return h.a >= 0 && h.b >= 0 && int64_t(h.a) + h.b <= d->num_children;
+  }
+  static bool is_wrapper(int k) {
+    return k == RT_TRANSLATE || k == RT_ROTATE_X || k == RT_ROTATE_Y || k == RT_ROTATE_Z || k == RT_SCALE;
+  }
+  static bool is_prim(int k) { return k == RT_SPHERE || k == RT_QUAD || k == RT_TRIANGLE; }
+
+  // -------------------------------------------------------------- prims
+  int add_sphere(int g) {
+    const rt_hittable& h = H(g);
+    DSphere s{};
+    s.cx = float(h.p[0]); s.cy = float(h.p[1]); s.cz = float(h.p[2]);
+    s.r = float(h.p[6]);
+    s.vx = float(h.p[3]); s.vy = float(h.p[4]); s.vz = float(h.p[5]);
+    s.mat = h.material;
+    S.spheres.push_back(s);
+    S.sphere_hidx.push_back(g);
+    return int(S.spheres.size()) - 1;
+  }
+  int add_quad(int g) {
+    const rt_hittable& h = H(g);
+    DQuad q{};
+    q.Qx = float(h.p[0]); q.Qy = float(h.p[1]); q.Qz = float(h.p[2]);
+    q.ux = float(h.p[3]); q.uy = float(h.p[4]); q.uz = float(h.p[5]);
+    q.vx = float(h.p[6]); q.vy = float(h.p[7]); q.vz = float(h.p[8]);
+    q.wx = float(h.p[9]); q.wy = float(h.p[10]); q.wz = float(h.p[11]);
+    q.nx = float(h.p[12]); q.ny = float(h.p[13]); q.nz = float(h.p[14]);
+    q.D = float(h.p[15]);
+    q.mat = h.material;
+    S.quads.push_back(q);
+    S.quad_hidx.push_back(g);
+    return int(S.quads.size()) - 1;
+  }
+  int add_tri(int g) {
+    const rt_hittable& h = H(g);
+    DTri t{};
+    float v0[3], v1[3], v2[3];
+    for (int a = 0; a < 3; ++a) { v0[a] = float(h.p[a]); v1[a] = float(h.p[3 + a]); v2[a] = float(h.p[6 + a]); }
+    for (int a = 0; a < 3; ++a) {
+      t.v0[a] = v0[a];
+      t.e1[a] = v1[a] - v0[a];   // edge1 := v1 - v0 (triangle.go:62), in fp32
+      t.e2[a] = v2[a] - v0[a];
+    }
+    DTriAux ax{};
+    ax.nx = float(h.p[9]); ax.ny = float(h.p[10]); ax.nz = float(h.p[11]);
+    ax.mat = h.material;
+    S.tris.push_back(t);
+    S.tri_aux.push_back(ax);
+    S.tri_hidx.push_back(g);
+    return int(S.tris.size()) - 1;
+  }
+  int prim_kind(int k) const {
+    return k == RT_SPHERE ? PK_SPHERE : k == RT_QUAD ? PK_QUAD : k == RT_TRIANGLE ? PK_TRI : -1;
+  }
+  int add_prim(int g) {
+    switch (H(g).kind) {
+      case RT_SPHERE: return add_sphere(g);
+      case RT_QUAD: return add_quad(g);
+      case RT_TRIANGLE: return add_tri(g);
+    }
+    return -1;
+  }
+
+  // Leaf over a list of primitive graph indices (BLAS level).  Homogeneous
+  // leaves index the primitive array directly; mixed ones go through refs.
+  uint32_t make_prim_leaf(const std::vector<int>& prims, int ntests) {
+    if (prims.empty()) return empty_leaf;
+    int k0 = H(prims[0]).kind;
+    bool homo = true;
+    for (int g : prims) {
+      if (!is_prim(H(g).kind)) { fail(RT_ERR_UNSUPPORTED, "BLAS leaf holds a non-primitive hittable"); return empty_leaf; }
+      if (H(g).kind != k0) homo = false;
+    }
+    DLeaf lf{};
+    if (homo) {
+      int first = -1;
+      for (int g : prims) { int i = add_prim(g); if (first < 0) first = i; }
+      lf.first = uint32_t(first);
+      lf.info = make_leaf_info(int(prims.size()), prim_kind(k0), ntests);
+    } else {
+      lf.first = uint32_t(S.refs.size());
+      for (int g : prims) {
+        int i = add_prim(g);
+        S.refs.push_back((uint32_t(prim_kind(H(g).kind)) << REF_SHIFT) | uint32_t(i));
+        S.ref_rank.push_back(0);
+        S.ref_top.push_back(-1);
+      }
+      lf.info = make_leaf_info(int(prims.size()), PK_MIXED, ntests);
+    }
+    if (prims.size() > 0xFFFF) { fail(RT_ERR_UNSUPPORTED, "leaf too large"); return empty_leaf; }
+    S.leaves.push_back(lf);
+    return (ITEM_LEAF << ITEM_SHIFT) | uint32_t(S.leaves.size() - 1);
+  }
+
+  std::vector<int> children_of(const rt_hittable& h) {
+    std::vector<int> c;
+    if (!child_range(h)) { fail(RT_ERR_INVALID, "bad child range"); return c; }
+    for (int i = 0; i < h.b; ++i) {
+      int g = d->children[h.a + i];
+      if (!valid_index(g)) { fail(RT_ERR_INVALID, "bad child index"); return {}; }
+      c.push_back(g);
+    }
+    return c;
+  }
+
+  // BLAS BVH node (graph BVH_NODE / leaf wrapper) -> item; box = graph bbox.
+  uint32_t blas_item(int g, int depth, int& maxdepth) {
+    if (depth > 200) { fail(RT_ERR_UNSUPPORTED, "BVH too deep"); return empty_leaf; }
+    if (depth > maxdepth) maxdepth = depth;
+    const rt_hittable& h = H(g);
+    if (h.kind == RT_BVH_NODE) {
+      if (!valid_index(h.a) || !valid_index(h.b)) { fail(RT_ERR_INVALID, "bad BVH child"); return empty_leaf; }
+      if (h.a == h.b) {  // BVHNode{leaf, leaf}: BVHLeaf.Hit runs twice
+        const rt_hittable& c = H(h.a);
+        if (c.kind == RT_BVH_LEAF) return make_prim_leaf(children_of(c), 2);
+        if (is_prim(c.kind)) return make_prim_leaf({h.a}, 2);
+        fail(RT_ERR_UNSUPPORTED, "BVH node with identical non-leaf children");
+        return empty_leaf;
+      }
+      int idx = int(S.nodes.size());
+      S.nodes.push_back(DNode{});
+      uint32_t li = blas_child(h.a, depth + 1, maxdepth);
+      uint32_t ri = blas_child(h.b, depth + 1, maxdepth);
+      DNode& n = S.nodes[idx];
+      Box lb, rb;
+      lb.merge(H(h.a).bbox);
+      rb.merge(H(h.b).bbox);
+      store_box(n.l, lb);
+      store_box(n.r, rb);
+      n.litem = li;
+      n.ritem = ri;
+      return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
+    }
+    if (h.kind == RT_BVH_LEAF) return make_prim_leaf(children_of(h), 1);
+    if (is_prim(h.kind)) return make_prim_leaf({g}, 1);
+    fail(RT_ERR_UNSUPPORTED, "unsupported hittable inside a BLAS BVH");
+    return empty_leaf;
+  }
+  uint32_t blas_child(int g, int depth, int& maxdepth) { return blas_item(g, depth, maxdepth); }
+
+  int build_blas(int g) {
+    auto it = blas_memo.find(g);
+    if (it != blas_memo.end()) return it->second;
+    const rt_hittable& h = H(g);
+    DBvh b{};
+    int depth = 0;
+    if (h.kind == RT_LIST) {          // HittableList.Hit: linear, no bbox test
+      b.root_item = make_prim_leaf(children_of(h), 1);
+      b.check_box = 0;
+    } else if (h.kind == RT_BVH_LEAF) {
+      b.root_item = make_prim_leaf(children_of(h), 1);
+      b.check_box = 0;
+    } else if (is_prim(h.kind)) {
+      b.root_item = make_prim_leaf({g}, 1);
+      b.check_box = 0;
+    } else if (h.kind == RT_BVH_NODE) {  // BVHNode.Hit tests its own bbox first
+      b.root_item = blas_item(g, 1, depth);
+      b.check_box = 1;
+    } else {
+      fail(RT_ERR_UNSUPPORTED, "unsupported BLAS root kind " + std::to_string(h.kind));
+      return -1;
+    }
+    Box bx;
+    bx.merge(h.bbox);
+    store_box(b.box, bx);
+    if (depth > S.blas_depth) S.blas_depth = depth;
+    S.blas.push_back(b);
+    int id = int(S.blas.size()) - 1;
+    blas_memo[g] = id;
+    return id;
+  }
+
+  // Collect a wrapper chain starting at g (outermost first); returns inner.
+  int make_instance(int g) {
+    DInstance in{};
+    int cur = g;
+    while (is_wrapper(H(cur).kind)) {
+      if (in.nwrap >= MAX_WRAP) { fail(RT_ERR_UNSUPPORTED, "transform chain too long"); return -1; }
+      const rt_hittable& w = H(cur);
+      int k = in.nwrap++;
+      switch (w.kind) {
+        case RT_TRANSLATE: in.kind[k] = W_TRANSLATE; break;
+        case RT_ROTATE_X: in.kind[k] = W_ROT_X; break;
+        case RT_ROTATE_Y: in.kind[k] = W_ROT_Y; break;
+        case RT_ROTATE_Z: in.kind[k] = W_ROT_Z; break;
+        case RT_SCALE: in.kind[k] = W_SCALE; break;
+      }
+      for (int j = 0; j < 6; ++j) in.prm[k][j] = float(w.p[j]);
+      if (!valid_index(w.a)) { fail(RT_ERR_INVALID, "bad wrapper child"); return -1; }
+      cur = w.a;
+    }
+    int bl = build_blas(cur);
+    if (bl < 0) return -1;
+    in.blas = bl;
+    S.instances.push_back(in);
+    return int(S.instances.size()) - 1;
+  }
+
+  int vol_id(int g) {
+    auto it = vol_ids.find(g);
+    if (it != vol_ids.end()) return it->second;
+    return -1;
+  }
+
+  // Top-level object -> ref (world prims, instances, volumes).
+  bool add_object_ref(int g, int rank) {
+    const rt_hittable& h = H(g);
+    uint32_t ref = 0;
+    if (h.kind == RT_SPHERE || h.kind == RT_QUAD || h.kind == RT_TRIANGLE) {
+      int i = add_prim(g);
+      ref = (uint32_t(prim_kind(h.kind)) << REF_SHIFT) | uint32_t(i);
+    } else if (h.kind == RT_VOLUME) {
+      if (!valid_index(h.a)) return fail(RT_ERR_INVALID, "bad volume boundary");
+      int inst = make_instance(h.a);
+      if (inst < 0) return false;
+      const DBvh& bb = S.blas[S.instances[inst].blas];
+      if ((bb.root_item >> ITEM_SHIFT) != ITEM_LEAF)
+        return fail(RT_ERR_UNSUPPORTED, "volume boundary must be a list/primitive (not a BVH)");
+      DVolume v{};
+      v.boundary = inst;
+      v.neg_inv_density = float(h.p[0]);
+      v.mat = h.material;
+      v.vol_id = vol_id(g);
+      S.volumes.push_back(v);
+      S.volume_hidx.push_back(g);
+      ref = (uint32_t(PK_VOLUME) << REF_SHIFT) | uint32_t(S.volumes.size() - 1);
+    } else if (is_wrapper(h.kind) || h.kind == RT_LIST || h.kind == RT_BVH_NODE || h.kind == RT_BVH_LEAF) {
+      int cur = g;
+      while (is_wrapper(H(cur).kind)) cur = H(cur).a;
+      if (!valid_index(cur)) return fail(RT_ERR_INVALID, "bad wrapper child");
+      if (H(cur).kind == RT_VOLUME || H(cur).kind == RT_PLANE)
+        return fail(RT_ERR_UNSUPPORTED, "transformed volume/plane not supported");
+      int inst = make_instance(g);
+      if (inst < 0) return false;
+      ref = (uint32_t(PK_INSTANCE) << REF_SHIFT) | uint32_t(inst);
+    } else {
+      return fail(RT_ERR_UNSUPPORTED, "unsupported top-level hittable kind " + std::to_string(h.kind));
+    }
+    S.refs.push_back(ref);
+    S.ref_rank.push_back(rank);
+    S.ref_top.push_back(g);
+    return true;
+  }
+
+  // World leaf: objects in order; planes lifted out (DFS rank kept).
+  uint32_t tlas_leaf(const std::vector<int>& objs, int ntests, Box& box) {
+    std::vector<int> ranks(objs.size());
+    for (size_t i = 0; i < objs.size(); ++i) ranks[i] = rank_counter++;
+    int count = 0, ninst = 0;
+    for (size_t i = 0; i < objs.size(); ++i) {
+      int g = objs[i];
+      const rt_hittable& h = H(g);
+      if (h.kind == RT_PLANE) {
+        DPlane p{};
+        p.px = float(h.p[0]); p.py = float(h.p[1]); p.pz = float(h.p[2]);
+        p.nx = float(h.p[3]); p.ny = float(h.p[4]); p.nz = float(h.p[5]);
+        p.mat = h.material;
+        p.rank = ranks[i];
+        S.planes.push_back(p);
+        S.plane_hidx.push_back(g);
+        continue;
+      }
+      count++;
+      // Pre-build BLASes: mixed BLAS leaves append refs, and the refs of
+      // this world leaf must stay contiguous.
+      int cur = h.kind == RT_VOLUME ? h.a : g;
+      while (valid_index(cur) && is_wrapper(H(cur).kind)) cur = H(cur).a;
+      if (!is_prim(h.kind) && valid_index(cur) &&
+          (H(cur).kind == RT_LIST || H(cur).kind == RT_BVH_NODE || H(cur).kind == RT_BVH_LEAF))
+        build_blas(cur);
+      if (status) return empty_leaf;
+    }
+    uint32_t first = uint32_t(S.refs.size());
+    for (size_t i = 0; i < objs.size(); ++i) {
+      int g = objs[i];
+      const rt_hittable& h = H(g);
+      if (h.kind == RT_PLANE) continue;
+      if (!add_object_ref(g, ranks[i])) return empty_leaf;
+      if ((S.refs.back() >> REF_SHIFT) == uint32_t(PK_INSTANCE)) ninst++;
+      box.merge(h.bbox);
+    }
+    if (uint32_t(S.refs.size()) - first != uint32_t(count)) {
+      fail(RT_ERR_INVALID, "internal: non-contiguous world leaf refs");
+      return empty_leaf;
+    }
+    if (count == 0) return empty_leaf;
+    if (ninst > 8) { fail(RT_ERR_UNSUPPORTED, "more than 8 instances in one world leaf"); return empty_leaf; }
+    if (ninst > max_leaf_inst) max_leaf_inst = ninst;
+    DLeaf lf{};
+    lf.first = first;
+    lf.info = make_leaf_info(count, PK_MIXED, ntests);
+    S.leaves.push_back(lf);
+    return (ITEM_LEAF << ITEM_SHIFT) | uint32_t(S.leaves.size() - 1);
+  }
+  int max_leaf_inst = 0;
+
+  // World BVH node -> item, refit box (planes excluded).
+  uint32_t tlas_item(int g, int depth, Box& box) {
+    if (depth > 200) { fail(RT_ERR_UNSUPPORTED, "world BVH too deep"); return empty_leaf; }
+    if (depth > S.tlas_depth) S.tlas_depth = depth;
+    const rt_hittable& h = H(g);
+    if (h.kind == RT_BVH_NODE) {
+      if (!valid_index(h.a) || !valid_index(h.b)) { fail(RT_ERR_INVALID, "bad BVH child"); return empty_leaf; }
+      if (h.a == h.b) {
+        const rt_hittable& c = H(h.a);
+        if (c.kind == RT_BVH_LEAF) return tlas_leaf(children_of(c), 2, box);
+        if (c.kind == RT_BVH_NODE) { fail(RT_ERR_UNSUPPORTED, "BVH node with identical subtree children"); return empty_leaf; }
+        return tlas_leaf({h.a}, 2, box);
+      }
+      int idx = int(S.nodes.size());
+      S.nodes.push_back(DNode{});
+      Box lb, rb;
+      uint32_t li = tlas_item(h.a, depth + 1, lb);
+      uint32_t ri = tlas_item(h.b, depth + 1, rb);
+      DNode& n = S.nodes[idx];
+      store_box(n.l, lb);
+      store_box(n.r, rb);
+      n.litem = lb.empty() ? empty_leaf : li;
+      n.ritem = rb.empty() ? empty_leaf : ri;
+      box.merge(lb);
+      box.merge(rb);
+      return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
+    }
+    if (h.kind == RT_BVH_LEAF || h.kind == RT_LIST) return tlas_leaf(children_of(h), 1, box);
+    return tlas_leaf({g}, 1, box);
+  }
+
+  void materials() {
+    for (int i = 0; i < d->num_materials; ++i) {
+      const rt_material& m = d->materials[i];
+      DMaterial o{};
+      o.kind = m.kind;
+      o.tex = m.texture;
+      o.fuzz = float(m.fuzz);
+      o.ior = float(m.refraction_index);
+      for (int a = 0; a < 3; ++a) o.albedo[a] = float(m.albedo[a]);
+      if (m.kind < RT_LAMBERTIAN || m.kind > RT_ISOTROPIC) { fail(RT_ERR_UNSUPPORTED, "unknown material kind"); return; }
+      if ((m.kind == RT_LAMBERTIAN || m.kind == RT_DIFFUSE_LIGHT || m.kind == RT_ISOTROPIC) &&
+          (m.texture < 0 || m.texture >= d->num_textures)) { fail(RT_ERR_INVALID, "bad texture index"); return; }
+      S.materials.push_back(o);
+    }
+    for (int i = 0; i < d->num_textures; ++i) {
+      const rt_texture& t = d->textures[i];
+      DTexture o{};
+      o.kind = t.kind;
+      if (t.kind == RT_TEX_SOLID) {
+        for (int a = 0; a < 3; ++a) o.even[a] = o.odd[a] = float(t.albedo[a]);
+      } else if (t.kind == RT_TEX_CHECKER) {
+        if (t.even < 0 || t.even >= d->num_textures || t.odd < 0 || t.odd >= d->num_textures ||
+            d->textures[t.even].kind != RT_TEX_SOLID || d->textures[t.odd].kind != RT_TEX_SOLID) {
+          fail(RT_ERR_UNSUPPORTED, "checker texture with non-solid sub-textures");
+          return;
+        }
+        o.inv_scale = float(t.inv_scale);
+        for (int a = 0; a < 3; ++a) {
+          o.even[a] = float(d->textures[t.even].albedo[a]);
+          o.odd[a] = float(d->textures[t.odd].albedo[a]);
+        }
+      } else {
+        fail(RT_ERR_UNSUPPORTED, "unsupported texture kind");
+        return;
+      }
+      S.textures.push_back(o);
+    }
+  }
+
+  void lights() {
+    for (int i = 0; i < d->num_lights; ++i) {
+      int g = d->lights[i];
+      if (!valid_index(g)) { fail(RT_ERR_INVALID, "bad light index"); return; }
+      const rt_hittable& h = H(g);
+      DLight l{};
+      if (h.kind == RT_QUAD) {          // camera.go:616-619: only *Quad lights
+        for (int a = 0; a < 3; ++a) {
+          l.Q[a] = float(h.p[a]);
+          l.u[a] = float(h.p[3 + a]);
+          l.v[a] = float(h.p[6 + a]);
+          l.n[a] = float(h.p[12 + a]);
+        }
+        l.mat = h.material;
+        l.is_quad = 1;
+      }
+      S.lights.push_back(l);
+    }
+  }
+
+  // HDRIEnvironment.BuildDistribution (hdri.go:145-224), fp64, then fp32 tables.
+  void environment() {
+    const rt_environment* e = d->environment;
+    if (!e) return;
+    if (!e->rgb || e->width <= 0 || e->height <= 0) return;  // IsValid() false
+    const int W = e->width, H = e->height;
+    S.env_valid = 1;
+    S.env_w = W;
+    S.env_h = H;
+    S.env_rotation = float(e->rotation);
+    S.env_use_is = e->use_importance_sampling ? 1 : 0;
+    S.env_texels.assign(size_t(W) * H * 4, 0.f);
+    for (size_t i = 0; i < size_t(W) * H; ++i)
+      for (int c = 0; c < 3; ++c) S.env_texels[i * 4 + c] = float(e->rgb[i * 3 + c]);
+    if (!S.env_use_is) return;
+    std::vector<double> pdf(size_t(W) * H), rows(H, 0.0), marg(H + 1), cond(size_t(H) * (W + 1));
+    double total = 0.0;
+    for (int y = 0; y < H; ++y) {
+      double v = (double(y) + 0.5) / double(H);
+      double theta = (0.5 - v) * M_PI;
+      double st = std::cos(theta);
+      cond[size_t(y) * (W + 1)] = 0.0;
+      for (int x = 0; x < W; ++x) {
+        size_t idx = size_t(y) * W + x;
+        const double* c = e->rgb + idx * 3;
+        double lum = 0.2126 * c[0] + 0.7152 * c[1] + 0.0722 * c[2];
+        double w = lum * st;
+        if (w < 0) w = 0;
+        pdf[idx] = w;
+        rows[y] += w;
+        total += w;
+        cond[size_t(y) * (W + 1) + x + 1] = cond[size_t(y) * (W + 1) + x] + w;
+      }
+    }
+    for (int y = 0; y < H; ++y)
+      if (rows[y] > 0)
+        for (int x = 0; x <= W; ++x) cond[size_t(y) * (W + 1) + x] /= rows[y];
+    marg[0] = 0;
+    for (int y = 0; y < H; ++y) marg[y + 1] = marg[y] + rows[y];
+    if (total > 0) {
+      for (int y = 0; y <= H; ++y) marg[y] /= total;
+      for (auto& p : pdf) p /= total;
+    }
+    S.env_total_power = float(total);
+    S.env_pdf.assign(pdf.begin(), pdf.end());
+    S.env_marginal.assign(marg.begin(), marg.end());
+    S.env_conditional.assign(cond.begin(), cond.end());
+  }
+
+  int run() {
+    if (!d || !d->hittables || d->num_hittables <= 0) { fail(RT_ERR_INVALID, "empty scene"); return status; }
+    if (!valid_index(d->root)) { fail(RT_ERR_INVALID, "bad root"); return status; }
+    if (d->num_children > 0 && !d->children) { fail(RT_ERR_INVALID, "children table missing"); return status; }
+    // volume ids in graph-index order (the oracle uses the same numbering)
+    int nv = 0;
+    for (int i = 0; i < d->num_hittables; ++i)
+      if (d->hittables[i].kind == RT_VOLUME) vol_ids[i] = nv++;
+    if (nv > 1024) { fail(RT_ERR_UNSUPPORTED, "too many volumes"); return status; }
+    for (int i = 0; i < d->num_hittables; ++i) {
+      const rt_hittable& h = d->hittables[i];
+      if ((is_prim(h.kind) || h.kind == RT_PLANE || h.kind == RT_VOLUME) &&
+          (h.material < 0 || h.material >= d->num_materials)) {
+        fail(RT_ERR_INVALID, "bad material index on hittable " + std::to_string(i));
+        return status;
+      }
+    }
+    materials();
+    if (status) return status;
+    // empty leaf record at index 0
+    S.leaves.push_back(DLeaf{0, make_leaf_info(0, PK_MIXED, 1)});
+    empty_leaf = (ITEM_LEAF << ITEM_SHIFT) | 0u;
+    Box root;
+    uint32_t ri = tlas_item(d->root, 1, root);
+    if (status) return status;
+    S.tlas.root_item = ri;
+    S.tlas.check_box = H(d->root).kind == RT_BVH_NODE ? 1 : 0;
+    store_box(S.tlas.box, root);
+    lights();
+    if (status) return status;
+    environment();
+    // stack: one pending far child per world level + pending instances in a
+    // leaf + the INST_END marker + one per BLAS level.
+    S.stack_needed = S.tlas_depth + max_leaf_inst + 1 + S.blas_depth + 2;
+    if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
+    if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27))
+      fail(RT_ERR_UNSUPPORTED, "scene too large for 28-bit indices");
+    return status;
+  }
+};
+
+}  // namespace
+
+int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err) {
+  out = HostScene{};
+  Flattener f(desc, out, err);
+  return f.run();
+}
+
+}  // namespace rtg

@@ -1,0 +1,48 @@
+// flatten.h — Go object graph (rt_scene_desc) -> flattened fp32 device layout.
+#pragma once
+#include <string>
+#include <vector>
+#include "../../include/rtgpu.h"
+#include "dev_layout.h"
+
+namespace rtg {
+
+struct HostScene {
+  std::vector<DNode> nodes;
+  std::vector<DLeaf> leaves;
+  std::vector<uint32_t> refs;
+  std::vector<int32_t> ref_rank;      // per ref (TLAS refs: DFS rank; others 0)
+  std::vector<int32_t> ref_top;       // per ref: top-level hittable index
+  std::vector<DSphere> spheres;
+  std::vector<int32_t> sphere_hidx;
+  std::vector<DQuad> quads;
+  std::vector<int32_t> quad_hidx;
+  std::vector<DTri> tris;
+  std::vector<DTriAux> tri_aux;
+  std::vector<int32_t> tri_hidx;
+  std::vector<DPlane> planes;
+  std::vector<int32_t> plane_hidx;
+  std::vector<DInstance> instances;
+  std::vector<DBvh> blas;
+  std::vector<DVolume> volumes;
+  std::vector<int32_t> volume_hidx;
+  std::vector<DMaterial> materials;
+  std::vector<DTexture> textures;
+  std::vector<DLight> lights;
+  DBvh tlas{};
+  // environment
+  int env_valid = 0, env_w = 0, env_h = 0, env_use_is = 0;
+  float env_rotation = 0.f, env_total_power = 0.f;
+  std::vector<float> env_texels, env_pdf, env_marginal, env_conditional;
+  int stack_needed = 0;
+  int tlas_depth = 0, blas_depth = 0;
+};
+
+// Returns RT_OK or an rt_status; `err` receives a message.
+int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err);
+
+// fp64 -> fp32 with outward rounding (bbox lower / upper bounds).
+float round_down(double x);
+float round_up(double x);
+
+}  // namespace rtg

@@ -1,0 +1,237 @@
+/*
+ * rtgpu.h — C-ABI drop-in boundary of the MI355X (gfx950) path tracer.
+ *
+ * The hot path it replaces is the per-pixel samples x bounces loop of
+ * byvfx/go-raytracing:
+ *   rt.BucketRenderer.renderBucketWithQuality   rt/bucket_renderer.go:257-301
+ *   rt.Camera.GetRay                            rt/camera.go:368-435
+ *   rt.Camera.RayColor / rayColorInternal       rt/camera.go:438-518
+ *   rt.Camera.sampleLightMIS/AreaLight/HDRI     rt/camera.go:538-678
+ * and everything those call (Hittable.Hit, Material.Scatter/Emitted/PDF,
+ * Texture.Value, HDRIEnvironment.Sample/SampleDirection/PDF).
+ *
+ * The Go host keeps building scenes with its own builders (scenes.go) and
+ * hands the object graph across this boundary once per render, flattened by
+ * a type switch over the concrete Go types (see INTEGRATION.md for the cgo
+ * binding and the in-package flattener).  The graph is copied before
+ * rt_scene_upload returns; C never retains caller memory.
+ *
+ * Every entry point sets the HIP device of its context itself (cgo calls may
+ * land on any OS thread).  Errors are int status codes (RT_OK == 0) plus a
+ * per-context message from rt_last_error(); no C++ exception crosses.
+ *
+ * Plain C types only: no torch, no HIP types in the signatures (the stream
+ * argument of the *_device entry points is an opaque hipStream_t).
+ */
+#ifndef RTGPU_H
+#define RTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+enum rt_status {
+  RT_OK = 0,
+  RT_ERR_INVALID = -1,     /* bad argument / malformed scene graph          */
+  RT_ERR_UNSUPPORTED = -2, /* Go type or nesting the GPU path does not take;
+                              the caller falls back to rt.BucketRenderer     */
+  RT_ERR_HIP = -3,         /* HIP runtime error (message in rt_last_error)  */
+  RT_ERR_OOM = -4,         /* device allocation failed                      */
+  RT_ERR_NO_SCENE = -5,    /* rt_render before rt_scene_upload              */
+  RT_ERR_DEVICE = -6       /* kernel-side failure (e.g. traversal stack)    */
+};
+
+/* ---- scene graph: one node per concrete rt.Hittable ------------------------
+ * Mirrors rt.Hittable (hittable.go:15-18).  `bbox` is the Go object's
+ * BoundingBox() as {xmin,xmax,ymin,ymax,zmin,zmax}; `p` holds the Go struct
+ * fields (float64) listed per kind.                                          */
+enum rt_hittable_kind {
+  RT_SPHERE = 1,      /* sphere.go:6-11   p[0..2]=Center.orig p[3..5]=Center.dir
+                                          (velocity) p[6]=Radius                */
+  RT_QUAD = 2,        /* quad.go:5-14     p[0..2]=Q p[3..5]=u p[6..8]=v
+                                          p[9..11]=w p[12..14]=normal p[15]=D   */
+  RT_TRIANGLE = 3,    /* triangle.go:8-14 p[0..2]=v0 p[3..5]=v1 p[6..8]=v2
+                                          p[9..11]=normal (unit)               */
+  RT_PLANE = 4,       /* plane.go:5-10    p[0..2]=Point p[3..5]=Normal (unit)  */
+  RT_LIST = 5,        /* hittable_list.go:3-6  children[a .. a+b)              */
+  RT_BVH_NODE = 6,    /* bvh.go:13-17     a=left b=right (a==b for the leaf
+                                          wrapper BVHNode{leaf,leaf}, bvh.go:141) */
+  RT_BVH_LEAF = 7,    /* bvh.go:21-24     children[a .. a+b)                   */
+  RT_TRANSLATE = 8,   /* transform.go:78-82   a=Obj p[0..2]=Offset             */
+  RT_ROTATE_X = 9,    /* transform.go:194-199 a=Obj p[0]=SinTheta p[1]=CosTheta */
+  RT_ROTATE_Y = 10,   /* transform.go:113-118 a=Obj p[0]=SinTheta p[1]=CosTheta */
+  RT_ROTATE_Z = 11,   /* transform.go:275-280 a=Obj p[0]=SinTheta p[1]=CosTheta */
+  RT_SCALE = 12,      /* transform.go:360-365 a=Obj p[0..2]=Factor p[3..5]=InvFactor */
+  RT_VOLUME = 13      /* volume.go:9-13   a=boundary p[0]=negInvDensity
+                                          material=phaseFunction (Isotropic)   */
+};
+
+typedef struct rt_hittable {
+  int32_t kind;     /* enum rt_hittable_kind                                 */
+  int32_t material; /* index into rt_scene_desc.materials (prims, volume)    */
+  int32_t a;        /* child / left / first (see kinds)                      */
+  int32_t b;        /* right / count (see kinds)                             */
+  double bbox[6];   /* BoundingBox(): xmin,xmax,ymin,ymax,zmin,zmax          */
+  double p[16];     /* kind-specific float64 fields                          */
+} rt_hittable;
+
+/* ---- materials (material.go:9-288) and textures (texture.go:5-77) -------- */
+enum rt_material_kind {
+  RT_LAMBERTIAN = 1,    /* material.go:33-80   texture                        */
+  RT_METAL = 2,         /* material.go:86-140  albedo, fuzz (already clamped ≤1) */
+  RT_DIELECTRIC = 3,    /* material.go:146-196 refraction_index               */
+  RT_DIFFUSE_LIGHT = 4, /* material.go:202-236 texture                        */
+  RT_ISOTROPIC = 5      /* material.go:243-278 texture                        */
+};
+
+typedef struct rt_material {
+  int32_t kind;
+  int32_t texture;  /* index into textures (Lambertian/DiffuseLight/Isotropic) */
+  double albedo[3]; /* Metal.Albedo                                           */
+  double fuzz;      /* Metal.Fuzz                                             */
+  double refraction_index; /* Dielectric.RefractionIndex                     */
+} rt_material;
+
+enum rt_texture_kind {
+  RT_TEX_SOLID = 1,  /* SolidColor, texture.go:9-11,43-45                    */
+  RT_TEX_CHECKER = 2 /* CheckerTexture, texture.go:13-17,47-77               */
+};
+
+typedef struct rt_texture {
+  int32_t kind;
+  int32_t even, odd; /* checker: texture indices (must be RT_TEX_SOLID)      */
+  double albedo[3];  /* solid colour                                         */
+  double inv_scale;  /* checker invScale                                     */
+} rt_texture;
+
+/* ---- HDRI environment (hdri.go:13-26, image_loader.go:17-24) ------------- */
+typedef struct rt_environment {
+  int32_t width, height;          /* ImageLoader dims                         */
+  const double* rgb;              /* ImageLoader.data, width*height*3 float64 */
+  double rotation;                /* radians (HDRIEnvironment.rotation)       */
+  int32_t use_importance_sampling;/* HDRIEnvironment.useImportanceSampling    */
+} rt_environment;
+
+typedef struct rt_scene_desc {
+  const rt_hittable* hittables;
+  int32_t num_hittables;
+  const int32_t* children;   /* child index table for RT_LIST / RT_BVH_LEAF   */
+  int32_t num_children;
+  int32_t root;              /* the world passed to NewBucketRenderer         */
+  const rt_material* materials;
+  int32_t num_materials;
+  const rt_texture* textures;
+  int32_t num_textures;
+  const int32_t* lights;     /* Camera.Lights (camera.go:38), hittable indices */
+  int32_t num_lights;
+  const rt_environment* environment; /* Camera.Environment or NULL (camera.go:39) */
+} rt_scene_desc;
+
+/* ---- camera: the state Camera.Initialize() leaves (camera.go:286-344) ---- */
+typedef struct rt_camera_desc {
+  int32_t image_width, image_height;
+  int32_t samples_per_pixel; /* Camera.SamplesPerPixel                       */
+  int32_t max_depth;         /* Camera.MaxDepth (PhantomHDRI primary test)   */
+  double center[3];          /* c.center                                     */
+  double pixel00[3];         /* c.pixel00Loc                                 */
+  double pixel_delta_u[3];
+  double pixel_delta_v[3];
+  double defocus_angle;      /* c.DefocusAngle (>0 enables the disk)         */
+  double defocus_disk_u[3];
+  double defocus_disk_v[3];
+  double background[3];      /* c.Background                                 */
+  int32_t use_sky_gradient;  /* c.UseSkyGradient                             */
+  int32_t phantom_hdri;      /* c.PhantomHDRI                                */
+  int32_t camera_motion;     /* c.CameraMotion (unsupported: must be 0)      */
+  int32_t free_camera;       /* c.FreeCamera   (unsupported: must be 0)      */
+} rt_camera_desc;
+
+/* ---- render call ----------------------------------------------------------- */
+typedef struct rt_bucket { int32_t x, y, width, height; } rt_bucket; /* bucket_renderer.go:22-27 */
+
+typedef struct rt_render_params {
+  int32_t samples_per_pixel; /* samplesForPass (bucket_renderer.go:175-191)  */
+  int32_t max_depth;         /* depthForPass                                 */
+  int32_t sample_offset;     /* first global sample index (RNG key)          */
+  uint32_t seed;             /* RNG seed (counter-based)      */
+  const rt_bucket* buckets;  /* NULL: the whole image                        */
+  int32_t num_buckets;
+  int32_t accumulate;        /* 1: add into accum; 0: overwrite bucket pixels */
+} rt_render_params;
+
+typedef struct rt_stats {
+  double kernel_ms;          /* device time of the render kernels            */
+  uint64_t samples;          /* pixels x samples rendered                    */
+} rt_stats;
+
+/* Per-sample traversal work counted by the instrumented kernel variant
+ * (feeds the algorithmic-bytes roofline).           */
+typedef struct rt_work_counts {
+  uint64_t samples;
+  uint64_t rays;             /* closest-hit rays (camera + scattered)        */
+  uint64_t shadow_rays;
+  uint64_t node_visits;      /* BVH2 node fetches (two child boxes each)     */
+  uint64_t sphere_tests, quad_tests, tri_tests, plane_tests;
+  uint64_t instance_visits, volume_tests;
+  uint64_t material_fetches, env_lookups;
+} rt_work_counts;
+
+/* Sizes of the flattened device scene (rt_scene_get_info). */
+typedef struct rt_scene_info {
+  int32_t nodes, leaves, refs, spheres, quads, triangles, planes;
+  int32_t instances, blases, volumes, materials, textures, lights;
+  int32_t stack_needed, tlas_depth, blas_depth;
+  int64_t device_bytes;
+} rt_scene_info;
+
+typedef struct rt_ctx rt_ctx;
+
+int rt_abi_version(void);
+
+/* NewBucketRenderer analogue: one context per device. */
+int rt_ctx_create(int device, rt_ctx** out);
+void rt_ctx_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+
+/* Flatten + upload the Go object graph (copied; caller memory not retained). */
+int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene);
+
+int rt_scene_get_info(const rt_ctx* ctx, rt_scene_info* out);
+
+/* Render the buckets into a caller-owned host buffer of width*height*3 float
+ * (sum of per-sample radiance, linear).  Blocks until done.               */
+int rt_render(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+              float* accum_rgb, rt_stats* stats);
+
+/* Same, into a device buffer (width*height*3 float) on `hip_stream`;
+ * asynchronous.  Used by the multi-GPU driver (tile shard + RCCL combine). */
+int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+                     float* accum_rgb_device, void* hip_stream);
+
+/* Instrumented run of the same kernel: traversal/prim counters. */
+int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+                  rt_work_counts* out);
+
+/* RGBA8 quantisation of an accumulated sum (bucket_renderer.go:276-285):
+ * c*(1/spp) -> LinearToGamma (utils.go:85-90) -> clamp [0,0.999] ->
+ * uint8(256*x).  Host buffers; computed on the device.                    */
+int rt_tonemap_rgba8(rt_ctx* ctx, const float* accum_rgb, int32_t width, int32_t height,
+                     int32_t samples_per_pixel, uint8_t* rgba_out);
+
+/* Parity probe: first-bounce closest hit of sample `sample` for every pixel.
+ * out_top = hittable index of the top-level object (child of the world BVH
+ * leaf), out_prim = hittable index of the primitive (== top for
+ * non-instanced objects), -1 on miss; out_t = hit distance.               */
+int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
+                    int32_t* out_top, int32_t* out_prim, float* out_t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTGPU_H */

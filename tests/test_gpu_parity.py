@@ -1,0 +1,156 @@
+"""GPU (HIP, via the C-ABI) vs CPU oracle parity.  Marked gpu.
+
+Tolerances (stated, BASELINE.json north_star):
+  * first-bounce closest-hit ids (top-level object, primitive): bit-exact vs the
+    oracle's fp32 mirror mode;
+  * radiance: image mean over pixels of the squared RGB error of the per-pixel
+    average radiance < 1e-4 vs the fp32 oracle (same counter RNG keys);
+  * RGBA8 quantisation: bit-exact given the same float sums.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LUCY = dict(lucy_rings=60, lucy_cols=80)
+SCENES = [
+    ("simple", dict(width=96)),
+    ("random", dict(width=96)),
+    ("cornell", dict(width=64)),
+    ("cornell-smoke", dict(width=64)),
+    ("cornell-lucy", dict(width=64, **LUCY)),
+    ("hdri-test", dict(width=96)),
+    ("hdri-nee", dict(width=96)),
+]
+
+
+def _scene(g, name, kw):
+    return g.Scene(name, **kw)
+
+
+@pytest.mark.parametrize("name,kw", SCENES, ids=[s[0] for s in SCENES])
+def test_primary_hits_bit_exact(g, O, ctx, name, kw):
+    s = _scene(g, name, kw)
+    cam = s.camera
+    ctx.upload(s.desc)
+    for sample in (0, 3):
+        tg, pg, t_g = ctx.primary_hits(cam, 1234, sample)
+        to, po, t_o = O.primary_hits(s.desc, cam, 1234, sample, fp32=True)
+        mism = np.flatnonzero((tg != to) | (pg != po))
+        # volumes draw log(U): libm vs ocml may differ by an ulp -> allow a
+        # vanishing fraction only for scenes with fog.
+        allowed = 0 if "cornell" not in name or name == "cornell-lucy" else max(1, tg.size // 2000)
+        assert mism.size <= allowed, f"{name}: {mism.size} mismatches, first {mism[:5]}"
+        same = (tg == to) & (pg == po) & (tg >= 0)
+        if name in ("simple", "random", "cornell-lucy", "hdri-test", "hdri-nee"):
+            assert np.array_equal(t_g[same], t_o[same].astype(np.float32)), f"{name}: hit t differs"
+        assert (tg >= 0).any()
+
+
+@pytest.mark.parametrize("name,kw", SCENES, ids=[s[0] for s in SCENES])
+def test_radiance_parity_fp32(g, O, ctx, name, kw):
+    s = _scene(g, name, kw)
+    cam = s.camera
+    spp = 8
+    ctx.upload(s.desc)
+    p = g.make_params(spp, cam.max_depth, seed=77)
+    gpu, _ = ctx.render(cam, p)
+    ref = O.render(s.desc, cam, p, fp32=True)
+    assert np.isfinite(gpu).all()
+    mse = float(np.mean((gpu.astype(np.float64) / spp - ref / spp) ** 2))
+    assert mse < 1e-4, f"{name}: mse {mse:.3e}"
+    assert gpu.mean() > 0
+
+
+@pytest.mark.parametrize("name,kw", SCENES[:3], ids=[s[0] for s in SCENES[:3]])
+def test_radiance_vs_fp64_reference(g, O, ctx, name, kw):
+    """fp32 GPU vs the fp64 restatement of the Go arithmetic: statistical."""
+    s = _scene(g, name, kw)
+    cam = s.camera
+    spp = 16
+    ctx.upload(s.desc)
+    p = g.make_params(spp, cam.max_depth, seed=5)
+    gpu, _ = ctx.render(cam, p)
+    ref = O.render(s.desc, cam, p, fp32=False)
+    a = gpu.astype(np.float64) / spp
+    b = ref / spp
+    assert abs(a.mean() - b.mean()) < 0.02 * max(b.mean(), 1e-3)
+    assert float(np.mean((a - b) ** 2)) < 1e-2
+
+
+def test_tonemap_bit_exact(g, O, ctx):
+    rng = np.random.default_rng(0)
+    acc = (rng.random((37, 53, 3)) * 3.0).astype(np.float32)
+    acc[0, 0] = [0.0, -1.0, np.nan]
+    acc[0, 1] = [1e9, 0.998001 * 4, 0.25 * 4]
+    for spp in (1, 4, 7):
+        assert np.array_equal(ctx.tonemap(acc, spp), O.tonemap(acc, spp))
+
+
+def test_deterministic_and_bucket_split(g, ctx):
+    s = g.Scene("cornell", width=64)
+    cam = s.camera
+    ctx.upload(s.desc)
+    p = g.make_params(6, 5, seed=9)
+    a, _ = ctx.render(cam, p)
+    b, _ = ctx.render(cam, p)
+    assert np.array_equal(a, b)
+    bk = g.generate_buckets(cam.image_width, cam.image_height, 32)
+    acc = np.zeros_like(a)
+    for half in (bk[: len(bk) // 2], bk[len(bk) // 2:]):
+        ctx.render(cam, g.make_params(6, 5, seed=9, buckets=half), acc)
+    np.testing.assert_allclose(acc, a, rtol=2e-6, atol=1e-6)
+
+
+def test_accumulate_sample_offset(g, ctx):
+    s = g.Scene("simple", width=64)
+    cam = s.camera
+    ctx.upload(s.desc)
+    full, _ = ctx.render(cam, g.make_params(8, 10, seed=3))
+    acc, _ = ctx.render(cam, g.make_params(4, 10, seed=3))
+    ctx.render(cam, g.make_params(4, 10, seed=3, sample_offset=4, accumulate=True), acc)
+    np.testing.assert_allclose(acc, full, rtol=1e-5, atol=1e-5)
+
+
+def test_overwrite_only_bucket_pixels(g, ctx):
+    s = g.Scene("simple", width=64)
+    cam = s.camera
+    ctx.upload(s.desc)
+    acc = np.full((cam.image_height, cam.image_width, 3), -7.0, np.float32)
+    ctx.render(cam, g.make_params(2, 10, seed=3, buckets=[(0, 0, 16, 8)]), acc)
+    assert (acc[:8, :16] != -7.0).all()
+    assert (acc[8:] == -7.0).all() and (acc[:, 16:] == -7.0).all()
+
+
+def test_camera_motion_unsupported(g, ctx):
+    s = g.Scene("simple", width=32)
+    cam = s.camera
+    ctx.upload(s.desc)
+    cam.camera_motion = 1
+    with pytest.raises(g.RTError) as e:
+        ctx.render(cam, g.make_params(1, 3))
+    assert e.value.code == -2
+
+
+def test_count_work(g, ctx):
+    s = g.Scene("cornell", width=48)
+    cam = s.camera
+    ctx.upload(s.desc)
+    w = ctx.count_work(cam, g.make_params(4, 5, seed=1))
+    n = cam.image_width * cam.image_height * 4
+    assert w["samples"] == n
+    assert w["rays"] >= n and w["node_visits"] > 0 and w["quad_tests"] > 0 and w["volume_tests"] > 0
+    assert w["shadow_rays"] > 0
+
+
+def test_bucket_renderer_three_passes(g, tmp_path):
+    s = g.Scene("cornell", width=64, spp=8)
+    r = g.BucketRenderer(s, 32, 8, 0, seed=1)
+    assert not r.is_completed()
+    r.render_all()
+    assert r.is_completed()
+    fb = r.framebuffer()
+    assert fb.shape == (64, 64, 4) and (fb[..., 3] == 255).all() and fb[..., :3].max() > 0
+    out = tmp_path / "image.png"
+    r.save_image(str(out))
+    assert out.stat().st_size > 64 * 64 * 4
