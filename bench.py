@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s (pixels x spp / s) of the path-tracing hot path.
+
+Workload (N=1 and every N): CornellBoxLucy (scenes.go:714-817) overridden to
+1200x675, 500 spp, depth 5 — the configuration BASELINE.json's roofline
+target is quoted on — with the deterministic synthetic 280K-triangle Lucy
+stand-in (the real mesh is a Git-LFS pointer).  One step =
+one full-quality render of the frame (every pixel x every sample), scene
+already resident in HBM, output a device float3 accumulation buffer.
+
+Multi-GPU (torchrun, one rank per GPU): the 32x32 buckets of the frame are
+dealt round-robin to ranks; each rank renders its buckets into a zeroed
+full-frame buffer, then one RCCL reduce(sum) to rank 0 combines them (each
+pixel has exactly one contributor).  Total work is fixed: strong scaling.
+
+Output: one JSON line on rank 0 (contract in the task statement), with
+`roofline` for the render kernel (algorithmic bytes per launch from the
+instrumented kernel's traversal counts x the per-unit sizes of SURVEY.md
+§8(d) / DESIGN.md, over the render kernel's HIP-event time measured on its
+stream) and `cpu_baseline` (the CPU oracle's fp64 restatement of the Go path,
+multithreaded, on a bounded sample of the same workload; rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic bytes per unit of work.
+BYTES = {
+    "node_visits": 64,       # one BVH2 node = two 32-B child boxes
+    "tri_tests": 36,         # v0, e1, e2 fp32
+    "sphere_tests": 32,
+    "quad_tests": 64,
+    "plane_tests": 32,
+    "instance_visits": 96,   # 3x4 affine + inverse (SURVEY: 96 B)
+    "volume_tests": 64,
+    "material_fetches": 32,
+    "env_lookups": 48,       # 4 texels x 12 B
+}
+ACCUM_BYTES_PER_SAMPLE = 12
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="cornell-lucy")
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--aspect", type=float, default=16.0 / 9.0)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=0, help="0: scene default")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-count", action="store_true", help="skip the instrumented count run")
+    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    import __graft_entry__ as ge
+    g = ge.load_package()
+
+    scene_kw = {}
+    if args.width:
+        scene_kw["width"] = args.width
+    if args.aspect:
+        scene_kw["aspect"] = args.aspect
+    if args.spp:
+        scene_kw["spp"] = args.spp
+    if args.depth:
+        scene_kw["max_depth"] = args.depth
+    t_build = time.time()
+    scene = g.Scene(args.scene, **scene_kw)
+    cam = scene.camera
+    W, H, spp, depth = cam.image_width, cam.image_height, cam.samples_per_pixel, cam.max_depth
+    ctx = g.Context(local if world > 1 else 0)
+    ctx.upload(scene.desc)
+    info = ctx.info()
+    t_build = time.time() - t_build
+
+    buckets = g.generate_buckets(W, H, 32)
+    mine = g.shard_buckets(buckets, rank, world)
+    params = g.make_params(spp, depth, seed=args.seed, buckets=mine)
+    accum = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    kernel_ms = []
+
+    def step(timed: bool):
+        accum.zero_()
+        ctx.render_device(cam, params, accum.data_ptr(), stream.cuda_stream)
+        if timed:
+            kernel_ms.append(ctx.last_render_kernel_ms())
+        if dist is not None:
+            dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step(False)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = W * H * spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+    img_ok = bool(torch.isfinite(accum).all().item()) if rank == 0 else True
+
+    roofline = None
+    work = None
+    if rank == 0 and not args.no_count:
+        work = ctx.count_work(cam, params)
+        alg = sum(BYTES[k] * work[k] for k in BYTES) + ACCUM_BYTES_PER_SAMPLE * work["samples"]
+        avg_s = float(np.mean(kernel_ms)) / 1e3
+        achieved = alg / avg_s / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}x{spp}_n{world}.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "render_kernel", "kernel_ms_avg": round(avg_s * 1e3, 3),
+                    "alg_bytes_per_launch": int(alg)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle_py as O
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpu_spp = args.cpu_spp
+        # bounded sample: every pixel of the same frame at cpu_spp samples,
+        # same scene/BVH/depth, fp64 (the reference's arithmetic)
+        cp = g.make_params(cpu_spp, depth, seed=args.seed)
+        tc = time.perf_counter()
+        O.render(scene.desc, cam, cp, fp32=False, threads=threads)
+        tcpu = time.perf_counter() - tc
+        cpu = {"value": round(W * H * cpu_spp / tcpu / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+               "kind": "port",
+               "sample": f"{args.scene} {W}x{H} x {cpu_spp} spp depth {depth} (fp64 C restatement of the Go path, "
+                         f"{threads} threads), {tcpu:.1f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": "Msamples/sec (pixels x SPP / s)",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic 280K-tri Lucy stand-in; scene geometry per scenes.go)",
+            "config": {"workload": f"{args.scene} {W}x{H} {spp}spp depth {depth}", "scene": args.scene,
+                       "width": W, "height": H, "spp": spp, "max_depth": depth,
+                       "parallelism": f"tiles-rr{world}", "buckets": len(buckets),
+                       "triangles": info.triangles, "bvh_nodes": info.nodes,
+                       "scene_build_s": round(t_build, 2), "image_finite": img_ok},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if work is not None:
+            line["work_per_sample"] = {k: round(v / max(work["samples"], 1), 3) for k, v in work.items()
+                                       if k != "samples"}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -136,6 +136,7 @@ def rtgpu() -> C.CDLL:
         lib.rt_render.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), C.POINTER(C.c_float),
                                   C.POINTER(RtStats)]
         lib.rt_render_device.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), P, P]
+        lib.rt_last_render_kernel_ms.argtypes = [P, C.POINTER(C.c_double)]
         lib.rt_count_work.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
                                       C.POINTER(RtWorkCounts)]
         lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
@@ -279,6 +280,14 @@ def generate_buckets(width: int, height: int, bucket_size: int = 32):
     return bs
 
 
+def shard_buckets(buckets, rank: int, world: int):
+    """Round-robin tile sharding across ranks (bucket k -> rank k mod world):
+    the centre-heavy cost of the centre-out bucket order is spread evenly
+    (SURVEY.md §8(e)).  The RNG is keyed by global pixel id, so the combined
+    frame is identical for any world size."""
+    return [b for i, b in enumerate(buckets) if i % world == rank]
+
+
 def make_params(spp: int, depth: int, seed: int = 1, sample_offset: int = 0, buckets=None, accumulate: bool = False):
     keep = None
     if buckets is not None:
@@ -336,6 +345,11 @@ class Context:
     def render_device(self, camera: RtCameraDesc, params: RtRenderParams, dev_ptr: int, stream: int = 0):
         self._check(self._lib.rt_render_device(self._h, C.byref(camera), C.byref(params), C.c_void_p(dev_ptr),
                                                C.c_void_p(stream)))
+
+    def last_render_kernel_ms(self) -> float:
+        ms = C.c_double()
+        self._check(self._lib.rt_last_render_kernel_ms(self._h, C.byref(ms)))
+        return ms.value
 
     def count_work(self, camera: RtCameraDesc, params: RtRenderParams) -> dict:
         w = RtWorkCounts()

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -15,6 +16,7 @@
 #include "dev_layout.h"
 #include "flatten.h"
 #include "render_launch.h"
+#include "wavefront.h"
 
 using namespace rtg;
 
@@ -38,6 +40,17 @@ struct rt_ctx {
   int4* tiles_pinned = nullptr;     // staging for async tile uploads
   size_t tiles_pinned_n = 0;
   hipEvent_t tiles_ev = nullptr;
+  hipEvent_t kev0 = nullptr, kev1 = nullptr;   // render kernel only
+  bool kev_recorded = false;
+  // wavefront state
+  DevBuf wstate, wq, wpix, wacc;
+  size_t wslots = 0;
+  uint32_t* probe_pinned = nullptr;
+  int num_cus = 0;
+  std::vector<uint32_t> pix_host;
+  uint32_t* pix_pinned = nullptr;
+  size_t pix_pinned_n = 0;
+  hipEvent_t pix_ev = nullptr;
 };
 
 namespace {
@@ -151,6 +164,95 @@ int make_tiles(rt_ctx* ctx, const rt_render_params* p, int W, int H, std::vector
   return RT_OK;
 }
 
+// Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
+// batches sized to keep ~4M paths in flight.
+int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const std::vector<int4>& tiles, float* d_out,
+                hipStream_t st, bool count, unsigned long long* host_counters, double* ms) {
+  std::vector<uint32_t>& px = ctx->pix_host;
+  px.clear();
+  for (const int4& t : tiles)
+    for (int y = t.y; y < t.y + t.w; ++y)
+      for (int x = t.x; x < t.x + t.z; ++x) px.push_back(uint32_t(y) * uint32_t(dc.width) + uint32_t(x));
+  const uint32_t npix = uint32_t(px.size());
+  const uint32_t spp = uint32_t(p->samples_per_pixel);
+  const size_t target = size_t(4) << 20;   // path slots per batch
+  uint32_t spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
+  const size_t nslots = size_t(spb) * npix;
+  int rc;
+  if (ctx->wslots < nslots) {
+    free_buf(ctx->wstate);
+    free_buf(ctx->wq);
+    if ((rc = ensure(ctx, ctx->wstate, nslots * 11 * sizeof(float4)))) return rc;
+    if ((rc = ensure(ctx, ctx->wq, nslots * 3 * sizeof(uint32_t) + 64))) return rc;
+    ctx->wslots = nslots;
+  }
+  if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->wacc, size_t(npix) * 3 * sizeof(double)))) return rc;
+  if ((rc = ensure(ctx, ctx->counters, 16 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
+  // pixel list through pinned staging (async-safe)
+  HIPCHK(hipEventSynchronize(ctx->pix_ev));
+  if (ctx->pix_pinned_n < npix) {
+    if (ctx->pix_pinned) (void)hipHostFree(ctx->pix_pinned);
+    ctx->pix_pinned = nullptr;
+    ctx->pix_pinned_n = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&ctx->pix_pinned), npix * sizeof(uint32_t)));
+    ctx->pix_pinned_n = npix;
+  }
+  std::memcpy(ctx->pix_pinned, px.data(), npix * sizeof(uint32_t));
+  HIPCHK(hipMemcpyAsync(ctx->wpix.p, ctx->pix_pinned, npix * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(ctx->pix_ev, st));
+  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), st));
+  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(unsigned long long), st));
+  WaveArgs a{};
+  float4* base = static_cast<float4*>(ctx->wstate.p);
+  const size_t S = ctx->wslots;
+  a.ray_o = base; a.ray_d = base + S; a.beta = base + 2 * S; a.L = base + 3 * S; a.hit = base + 4 * S;
+  a.sh_p = base + 5 * S; a.sh_da = base + 6 * S; a.sh_dh = base + 7 * S; a.pend_a = base + 8 * S;
+  a.pend_h = base + 9 * S; a.pbeta = base + 10 * S;
+  uint32_t* qb = static_cast<uint32_t*>(ctx->wq.p);
+  a.counts = qb;
+  a.shcount = qb + 2;
+  a.q0 = qb + 16;
+  a.q1 = a.q0 + S;
+  a.shq = a.q1 + S;
+  a.pixels = static_cast<const uint32_t*>(ctx->wpix.p);
+  a.npix = npix;
+  a.acc = static_cast<double*>(ctx->wacc.p);
+  a.seed = p->seed;
+  a.max_depth = p->max_depth;
+  a.counters = static_cast<unsigned long long*>(ctx->counters.p);
+  a.err = static_cast<int*>(ctx->errflag.p);
+  WavePlan plan{};
+  plan.spp = spp;
+  plan.samples_per_batch = spb;
+  plan.sample_offset = uint32_t(p->sample_offset);
+  plan.max_depth = p->max_depth;
+  plan.num_cus = ctx->num_cus;
+  plan.probe_host = ctx->probe_pinned;
+  const int stack = ctx->host.stack_needed <= 32 ? 32 : 64;
+  if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
+  HIPCHK(hipEventRecord(ctx->kev0, st));
+  HIPCHK(launch_wavefront(ctx->dscene, dc, a, plan, stack, count, d_out, p->accumulate ? 1 : 0, st));
+  HIPCHK(hipEventRecord(ctx->kev1, st));
+  ctx->kev_recorded = true;
+  if (ms) HIPCHK(hipEventRecord(ctx->ev1, st));
+  if (count || ms) {
+    HIPCHK(hipStreamSynchronize(st));
+    int flag = 0;
+    HIPCHK(hipMemcpy(&flag, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
+    if (ms) {
+      float f = 0.f;
+      HIPCHK(hipEventElapsedTime(&f, ctx->ev0, ctx->ev1));
+      *ms = f;
+    }
+    if (count)
+      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  }
+  return RT_OK;
+}
+
 // Shared render path: tiles -> render kernel -> fixed-order reduce into `out`.
 int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* p, float* d_out,
                 hipStream_t st, bool count, unsigned long long* host_counters, double* ms) {
@@ -165,6 +267,8 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
   rc = make_tiles(ctx, p, dc.width, dc.height, tiles);
   if (rc) return rc;
   if (tiles.empty()) return RT_OK;
+  static const bool use_mega = [] { const char* e = getenv("RTGPU_PATH"); return e && std::string(e) == "mega"; }();
+  if (!use_mega) return render_wave(ctx, dc, p, tiles, d_out, st, count, host_counters, ms);
   const int ntiles = int(tiles.size());
   const int spp = p->samples_per_pixel;
   // Enough workgroups to fill 256 CUs several times over; chunks of samples
@@ -207,7 +311,10 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
   w.err = static_cast<int*>(ctx->errflag.p);
   const int stack = ctx->host.stack_needed <= 32 ? 32 : 64;
   if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
+  HIPCHK(hipEventRecord(ctx->kev0, st));
   HIPCHK(launch_render(ctx->dscene, dc, w, stack, count, st));
+  HIPCHK(hipEventRecord(ctx->kev1, st));
+  ctx->kev_recorded = true;
   if (!count) HIPCHK(launch_reduce(w, dc.width, d_out, st));
   if (ms) HIPCHK(hipEventRecord(ctx->ev1, st));
   if (count || ms) {
@@ -242,7 +349,11 @@ int rt_ctx_create(int device, rt_ctx** out) {
   ctx->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->tiles_ev, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->tiles_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&ctx->kev0) != hipSuccess || hipEventCreate(&ctx->kev1) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->pix_ev, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->probe_pinned), 64) != hipSuccess ||
+      hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
     delete ctx;
     return RT_ERR_HIP;
   }
@@ -259,6 +370,12 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   free_buf(ctx->accum); free_buf(ctx->rgba); free_buf(ctx->probe);
   if (ctx->tiles_pinned) (void)hipHostFree(ctx->tiles_pinned);
   (void)hipEventDestroy(ctx->tiles_ev);
+  free_buf(ctx->wstate); free_buf(ctx->wq); free_buf(ctx->wpix); free_buf(ctx->wacc);
+  if (ctx->pix_pinned) (void)hipHostFree(ctx->pix_pinned);
+  if (ctx->probe_pinned) (void)hipHostFree(ctx->probe_pinned);
+  (void)hipEventDestroy(ctx->pix_ev);
+  (void)hipEventDestroy(ctx->kev0);
+  (void)hipEventDestroy(ctx->kev1);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
   (void)hipStreamDestroy(ctx->stream);
@@ -315,6 +432,7 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_planes = int(h.planes.size());
   d.num_lights = int(h.lights.size());
   d.stack_needed = h.stack_needed;
+  d.has_volumes = h.volumes.empty() ? 0 : 1;
   ctx->has_scene = true;
   return RT_OK;
 }
@@ -374,6 +492,17 @@ int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_par
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
   return render_impl(ctx, cam, params, accum_rgb_device, st, false, nullptr, nullptr);
+}
+
+int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms) {
+  if (!ctx || !ms) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->kev_recorded) return set_err(ctx, RT_ERR_INVALID, "no render recorded");
+  HIPCHK(hipEventSynchronize(ctx->kev1));
+  float f = 0.f;
+  HIPCHK(hipEventElapsedTime(&f, ctx->kev0, ctx->kev1));
+  *ms = f;
+  return RT_OK;
 }
 
 int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, rt_work_counts* out) {

@@ -184,7 +184,7 @@ struct DScene {
   int32_t num_planes;
   int32_t num_lights;
   int32_t stack_needed;
-  int32_t pad;
+  int32_t has_volumes;
 };
 
 struct DCamera {

@@ -1,0 +1,804 @@
+// device_common.h — device-side building blocks shared by every kernel of
+// the path (render.hip megakernel/probe, wavefront.hip pipeline).  See the
+// file comment of render.hip for the reference functions restated here.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dev_layout.h"
+
+namespace rtg {
+
+// ----------------------------------------------------------------------------
+// Vec3 (vec3.go) in fp32, same operation order as Go.
+// ----------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 scale(V3 v, float t) { return mk(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ V3 divs(V3 v, float t) { return scale(v, 1.0f / t); }
+__device__ __forceinline__ V3 neg(V3 v) { return mk(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float len2(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+__device__ __forceinline__ float len(V3 v) { return sqrtf(len2(v)); }
+__device__ __forceinline__ V3 unit(V3 v) {
+  float l = len(v);
+  if (l == 0.0f) return v;
+  return divs(v, l);
+}
+__device__ __forceinline__ bool near_zero(V3 v) {
+  const float s = 1e-8f;
+  return fabsf(v.x) < s && fabsf(v.y) < s && fabsf(v.z) < s;
+}
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
+__device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {
+  float c = dot(neg(uv), n);
+  float cos_t = c < 1.0f ? c : 1.0f;                       // math.Min(.., 1.0)
+  V3 perp = scale(add(uv, scale(n, cos_t)), eta);
+  V3 par = scale(n, -sqrtf(fabsf(1.0f - len2(perp))));
+  return add(perp, par);
+}
+__device__ __forceinline__ float gomin(float x, float y) {   // math.Min, NaN propagates
+  return !(x >= y) ? x : y;
+}
+__device__ __forceinline__ V3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+constexpr float kPi = 3.14159265358979323846f;
+
+// ----------------------------------------------------------------------------
+// Counter-based RNG (replaces the unseeded global math/rand, utils.go:18-20).
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t path_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
+  uint32_t k = lowbias32(seed ^ 0xA511E9B3u);
+  k = lowbias32(k ^ pixel);
+  return lowbias32(k + sample * 0x9E3779B9u);
+}
+__device__ __forceinline__ uint32_t ctr(uint32_t bounce, uint32_t dom, uint32_t idx) {
+  return (bounce << 16) | (dom << 12) | idx;
+}
+__device__ __forceinline__ float rnd(uint32_t key, uint32_t counter) {
+  uint32_t h = lowbias32(key ^ lowbias32(counter ^ 0x632BE5ABu));
+  return float(h >> 8) * 0x1p-24f;
+}
+
+// RandomUnitVector (vec3.go:45-54): rejection in the cube, 1e-160 < |p|^2 <= 1
+// (1e-160 is 0 in fp32).  RandomDoubleRange(-1,1) = -1 + 2*U (utils.go:22-24).
+__device__ __forceinline__ V3 random_unit_vector(uint32_t key, uint32_t bounce, uint32_t dom, uint32_t base) {
+  for (int k = 0; k < MAX_UNIT_TRIES; ++k) {
+    uint32_t c = ctr(bounce, dom, base + 3u * k);
+    V3 p = mk(-1.0f + 2.0f * rnd(key, c), -1.0f + 2.0f * rnd(key, c + 1u), -1.0f + 2.0f * rnd(key, c + 2u));
+    float l2 = len2(p);
+    if (0.0f < l2 && l2 <= 1.0f) return divs(p, sqrtf(l2));
+  }
+  return mk(0.0f, 0.0f, 1.0f);   // P(64 rejections) < 1e-20
+}
+
+// ----------------------------------------------------------------------------
+// Rays
+// ----------------------------------------------------------------------------
+struct TRay {
+  V3 o, d, inv;
+};
+__device__ __forceinline__ TRay make_tray(V3 o, V3 d) {
+  TRay r; r.o = o; r.d = d;
+  r.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // AABB.Hit adinv (aabb.go:64)
+  return r;
+}
+
+// AABB.Hit (aabb.go:59-116) on a {xmin,xmax,ymin,ymax,zmin,zmax} box.
+// Returns the clamped entry distance in tnear.
+__device__ __forceinline__ bool slab(float bmin, float bmax, float o, float inv, float& tmin, float& tmax) {
+  float t0 = (bmin - o) * inv;
+  float t1 = (bmax - o) * inv;
+  if (inv < 0.0f) { float s = t0; t0 = t1; t1 = s; }
+  if (t0 > tmin) tmin = t0;
+  if (t1 < tmax) tmax = t1;
+  return tmax > tmin;
+}
+__device__ __forceinline__ bool box_hit(float x0, float x1, float y0, float y1, float z0, float z1,
+                                        const TRay& r, float tmin, float tmax, float& tnear) {
+  bool a = slab(x0, x1, r.o.x, r.inv.x, tmin, tmax);
+  bool b = slab(y0, y1, r.o.y, r.inv.y, tmin, tmax);
+  bool c = slab(z0, z1, r.o.z, r.inv.z, tmin, tmax);
+  tnear = tmin;
+  return a && b && c;   // monotone: equivalent to the early-exit form
+}
+
+// ----------------------------------------------------------------------------
+// Primitive intersection (t only; the hit record is rebuilt for the winner)
+// ----------------------------------------------------------------------------
+// Sphere.Hit sphere.go:63-86.  Open interval (Surrounds).  Returns candidate
+// t = first root > tmin (the Go code tries root2 only if root1 fails).
+__device__ __forceinline__ bool sphere_t(const DSphere& s, V3 o, V3 d, float time, float tmin, float& t) {
+  V3 c = add(mk(s.cx, s.cy, s.cz), scale(mk(s.vx, s.vy, s.vz), time));
+  V3 oc = sub(c, o);
+  float a = len2(d);
+  float h = dot(d, oc);
+  float cc = len2(oc) - s.r * s.r;
+  float disc = h * h - a * cc;
+  if (disc < 0.0f) return false;
+  float sq = sqrtf(disc);
+  float root = (h - sq) / a;
+  if (!(tmin < root)) {
+    root = (h + sq) / a;
+    if (!(tmin < root)) return false;
+  }
+  t = root;
+  return true;
+}
+
+// Quad.Hit quad.go:44-84.  Closed interval (Contains), alpha/beta in [0,1].
+__device__ __forceinline__ bool quad_t(const DQuad& q, V3 o, V3 d, float tmin, float& t) {
+  V3 n = mk(q.nx, q.ny, q.nz);
+  float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return false;
+  float tt = (q.D - dot(n, o)) / denom;
+  if (!(tmin <= tt)) return false;        // upper bound checked by the caller
+  V3 p = add(o, scale(d, tt));
+  V3 ph = sub(p, mk(q.Qx, q.Qy, q.Qz));
+  V3 w = mk(q.wx, q.wy, q.wz);
+  float alpha = dot(w, cross(ph, mk(q.vx, q.vy, q.vz)));
+  float beta = dot(w, cross(mk(q.ux, q.uy, q.uz), ph));
+  if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
+  t = tt;
+  return true;
+}
+
+// Triangle.Hit triangle.go:57-104 (Moller-Trumbore), closed interval.
+__device__ __forceinline__ bool tri_t(const DTri& tr, V3 o, V3 d, float tmin, float& t) {
+  V3 e1 = ld3(tr.e1), e2 = ld3(tr.e2);
+  V3 h = cross(d, e2);
+  float a = dot(e1, h);
+  if (fabsf(a) < 1e-8f) return false;
+  float f = 1.0f / a;
+  V3 s = sub(o, ld3(tr.v0));
+  float u = f * dot(s, h);
+  if (u < 0.0f || u > 1.0f) return false;
+  V3 q = cross(s, e1);
+  float v = f * dot(d, q);
+  if (v < 0.0f || u + v > 1.0f) return false;
+  float tt = f * dot(e2, q);
+  if (!(tmin <= tt)) return false;
+  t = tt;
+  return true;
+}
+
+// Plane.Hit plane.go:24-42, open interval.
+__device__ __forceinline__ bool plane_t(const DPlane& p, V3 o, V3 d, float tmin, float& t) {
+  V3 n = mk(p.nx, p.ny, p.nz);
+  float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return false;
+  float tt = dot(sub(mk(p.px, p.py, p.pz), o), n) / denom;
+  if (!(tmin < tt)) return false;
+  t = tt;
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// Transform wrapper chain (transform.go), outermost wrapper first.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void wrap_ray(int kind, const float* p, V3& o, V3& d) {
+  switch (kind) {
+    case W_TRANSLATE: o = sub(o, mk(p[0], p[1], p[2])); break;                    // :94
+    case W_ROT_Y: {                                                                  // :163-167
+      float s = p[0], c = p[1];
+      V3 no = o, nd = d;
+      no.x = c * o.x - s * o.z; no.z = s * o.x + c * o.z;
+      nd.x = c * d.x - s * d.z; nd.z = s * d.x + c * d.z;
+      o = no; d = nd; break;
+    }
+    case W_ROT_X: {                                                                  // :233-237
+      float s = p[0], c = p[1];
+      V3 no = o, nd = d;
+      no.y = c * o.y - s * o.z; no.z = s * o.y + c * o.z;
+      nd.y = c * d.y - s * d.z; nd.z = s * d.y + c * d.z;
+      o = no; d = nd; break;
+    }
+    case W_ROT_Z: {                                                                  // :314-318
+      float s = p[0], c = p[1];
+      V3 no = o, nd = d;
+      no.x = c * o.x - s * o.y; no.y = s * o.x + c * o.y;
+      nd.x = c * d.x - s * d.y; nd.y = s * d.x + c * d.y;
+      o = no; d = nd; break;
+    }
+    case W_SCALE:                                                                    // :409-418
+      o = mk(o.x * p[3], o.y * p[4], o.z * p[5]);
+      d = mk(d.x * p[3], d.y * p[4], d.z * p[5]);
+      break;
+    default: break;
+  }
+}
+// Back-map of the hit point and normal (inner wrapper first).
+__device__ __forceinline__ void unwrap_hit(int kind, const float* p, V3& P, V3& N) {
+  switch (kind) {
+    case W_TRANSLATE: P = add(P, mk(p[0], p[1], p[2])); break;                     // :100
+    case W_ROT_Y: {                                                                  // :175-184
+      float s = p[0], c = p[1];
+      V3 q = P, m = N;
+      q.x = c * P.x + s * P.z; q.z = -s * P.x + c * P.z;
+      m.x = c * N.x + s * N.z; m.z = -s * N.x + c * N.z;
+      P = q; N = m; break;
+    }
+    case W_ROT_X: {                                                                  // :243-251 (as written)
+      float s = p[0], c = p[1];
+      V3 q = P, m = N;
+      q.y = c * P.y - s * P.z; q.z = s * P.y + c * P.z;
+      m.y = c * N.y - s * N.z; m.z = s * N.y + c * N.z;
+      P = q; N = m; break;
+    }
+    case W_ROT_Z: {                                                                  // :324-332 (as written)
+      float s = p[0], c = p[1];
+      V3 q = P, m = N;
+      q.x = c * P.x - s * P.y; q.y = s * P.x + c * P.y;
+      m.x = c * N.x - s * N.y; m.y = s * N.x + c * N.y;
+      P = q; N = m; break;
+    }
+    case W_SCALE:                                                                    // :426-437
+      P = mk(P.x * p[0], P.y * p[1], P.z * p[2]);
+      N = unit(mk(N.x * p[3], N.y * p[4], N.z * p[5]));
+      break;
+    default: break;
+  }
+}
+__device__ __forceinline__ void to_object(const DInstance& in, V3& o, V3& d) {
+  for (int i = 0; i < in.nwrap; ++i) wrap_ray(in.kind[i], in.prm[i], o, d);
+}
+
+// ----------------------------------------------------------------------------
+// Closest-hit state and the tie rule: among equal t, the
+// reference's left-first DFS keeps the LAST closed-interval primitive
+// (Contains: quads, triangles, volumes) or else the FIRST open one
+// (Surrounds: spheres, planes).  Keys make that order-independent.
+// ----------------------------------------------------------------------------
+struct Best {
+  float t;
+  int kind;      // PK_*; 0 = none
+  int idx;       // prim / volume / plane index
+  int inst;      // instance id or -1
+  int refpos;    // TLAS ref position, or -1-plane for planes
+  int primpos;   // position inside the instance BLAS (rank), 0 otherwise
+};
+
+__device__ __forceinline__ bool closed_kind(int k) { return k == PK_QUAD || k == PK_TRI || k == PK_VOLUME; }
+
+__device__ __forceinline__ int obj_rank(const DScene& sc, int refpos) {
+  return refpos >= 0 ? sc.ref_rank[refpos] : sc.planes[-1 - refpos].rank;
+}
+// Is candidate (kind, refpos, primpos) preferred over the best at equal t?
+// Rare (exact float ties), scalar arguments only.
+__device__ __forceinline__ bool tie_wins(const DScene& sc, int kind, int refpos, int primpos, int bkind, int brefpos,
+                                         int bprimpos) {
+  const bool cc = closed_kind(kind), bc = closed_kind(bkind);
+  if (cc != bc) return cc;
+  const int rc = obj_rank(sc, refpos), rb = obj_rank(sc, brefpos);
+  if (rc == rb && primpos == bprimpos) return false;
+  const bool later = (rc > rb) || (rc == rb && primpos > bprimpos);
+  return cc ? later : !later;
+}
+__device__ __forceinline__ bool accept(const DScene& sc, float t, int kind, int refpos, int primpos, const Best& b) {
+  if (t < b.t) return true;
+  if (t == b.t && b.kind != 0) return tie_wins(sc, kind, refpos, primpos, b.kind, b.refpos, b.primpos);
+  return false;
+}
+
+// Work counters for the instrumented variant (rt_count_work).
+struct Cnt {
+  uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env;
+};
+
+// Volume.Hit (volume.go:34-79) against a boundary given as an instance chain
+// over a list leaf.  ntests = how many times the enclosing leaf calls Hit
+// (2 for the BVHNode{leaf,leaf} wrapper): the reference then keeps the
+// smaller of the independent free-flight draws, i.e. U = max(U_1..U_n).
+template <bool kCount>
+__device__ bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, float time,
+                           float tmin, float tmax, int ntests, uint32_t key, uint32_t bounce,
+                           uint32_t dom, float& t_out, Cnt& cnt) {
+  const DInstance& bi = sc.instances[vol.boundary];
+  V3 o = wo, d = wd;
+  to_object(bi, o, d);
+  const DBvh& bb = sc.blas[bi.blas];
+  DLeaf lf = sc.leaves[bb.root_item & ITEM_MASK];
+  int n = leaf_count(lf.info), kind = leaf_kind(lf.info);
+  // rec1: closest over the universe interval; rec2: closest over (t1+1e-4, inf).
+  float t1 = __builtin_inff(), t2 = __builtin_inff();
+  bool h1 = false, h2 = false;
+  for (int pass = 0; pass < 2; ++pass) {
+    float lo = pass == 0 ? -__builtin_inff() : t1 + 0.0001f;
+    float closest = __builtin_inff();
+    bool found = false;
+    for (int k = 0; k < n; ++k) {
+      int pk = kind; uint32_t pi = lf.first + k;
+      if (kind == PK_MIXED) { uint32_t r = sc.refs[pi]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
+      float t;
+      bool ok = false;
+      if (pk == PK_QUAD) { ok = quad_t(sc.quads[pi], o, d, lo, t) && t <= closest; }
+      else if (pk == PK_TRI) { ok = tri_t(sc.tris[pi], o, d, lo, t) && t <= closest; }
+      else if (pk == PK_SPHERE) { ok = sphere_t(sc.spheres[pi], o, d, time, lo, t) && t < closest; }
+      if (ok) { closest = t; found = true; }
+    }
+    if (pass == 0) { h1 = found; t1 = closest; if (!h1) break; }
+    else { h2 = found; t2 = closest; }
+  }
+  if (kCount) cnt.vol++;
+  if (!h1 || !h2) return false;
+  if (t1 < tmin) t1 = tmin;
+  if (t2 > tmax) t2 = tmax;
+  if (t1 >= t2) return false;
+  if (t1 < 0.0f) t1 = 0.0f;
+  float rl = len(wd);
+  float dist = (t2 - t1) * rl;
+  float u = 0.0f;
+  for (int p = 0; p < ntests; ++p) {
+    float up = rnd(key, ctr(bounce, dom, uint32_t(vol.vol_id) * 4u + uint32_t(p)));
+    u = up > u ? up : u;
+  }
+  float hd = vol.neg_inv_density * logf(u);
+  if (hd > dist) return false;
+  t_out = t1 + hd / rl;
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// BVH traversal ("while-while", Aila & Laine 2009, adapted to wave64): one
+// loop for the world BVH and instance BLASes (ray switched to object space on
+// ITEM_INSTANCE, restored on ITEM_INST_END).  Lanes walk internal nodes
+// together and postpone the first leaf they reach; leaves are processed once
+// every lane of the wave holds one (ballot), which keeps the SIMD lanes in the
+// same code section.  Result = closest hit with the DFS tie rule, independent
+// of visiting order (BVHNode.Hit bvh.go:219-239 visits left-first).
+//   kAny = false: closest hit in [tmin, tmax) with the tie rule.
+//   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
+// ----------------------------------------------------------------------------
+constexpr uint32_t ITEM_NONE = 0xFFFFFFFFu;
+constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the stack"
+
+template <bool kAny, bool kCount, bool kVol = true>
+__device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin, float tmax,
+                         uint32_t* stk, int stride, int cap, Best& best, uint32_t key,
+                         uint32_t bounce, uint32_t voldom, Cnt& cnt, int* err) {
+  best.t = tmax; best.kind = 0; best.idx = -1; best.inst = -1; best.refpos = 0; best.primpos = 0;
+  // Planes (pulled out of the BVH: universe bbox).
+  for (int i = 0; i < sc.num_planes; ++i) {
+    float t;
+    if (kCount) cnt.plane++;
+    if (plane_t(sc.planes[i], wo, wd, tmin, t)) {
+      if (kAny) { if (t < tmax) return true; }
+      else if (accept(sc, t, PK_PLANE, -1 - i, 0, best)) {
+        best.t = t; best.kind = PK_PLANE; best.idx = i; best.inst = -1; best.refpos = -1 - i; best.primpos = 0;
+      }
+    }
+  }
+  TRay cr = make_tray(wo, wd);
+  int cur_inst = -1, cur_ref = -1;
+  float tn;
+  if (sc.tlas.check_box &&
+      !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
+               cr, tmin, kAny ? tmax : best.t, tn))
+    return kAny ? false : best.kind != 0;
+  int sp = 0;
+  uint32_t item = sc.tlas.root_item, lf = ITEM_NONE;
+  auto pop = [&]() -> uint32_t { if (sp == 0) return ITEM_NONE; --sp; return stk[sp * stride]; };
+  auto push = [&](uint32_t v) -> bool {
+    if (sp >= cap) { *err = 1; return false; }
+    stk[sp * stride] = v; ++sp; return true;
+  };
+  // park a non-node item in lf (leaves allow speculative traversal to go on)
+  auto postpone = [&]() {
+    lf = item;
+    item = ((lf >> ITEM_SHIFT) == ITEM_LEAF) ? pop() : ITEM_POP;
+  };
+  if ((item >> ITEM_SHIFT) != ITEM_NODE) postpone();
+  while (item != ITEM_NONE || lf != ITEM_NONE) {
+    // ---------------- phase 1: internal nodes
+    while (item < ITEM_POP && (item >> ITEM_SHIFT) == ITEM_NODE) {
+      const float4* np = reinterpret_cast<const float4*>(sc.nodes + (item & ITEM_MASK));
+      const float4 a = np[0], b = np[1], c = np[2];
+      const uint4 m = reinterpret_cast<const uint4*>(np)[3];
+      if (kCount) cnt.nodes++;
+      const float hi = kAny ? tmax : best.t;
+      float tl, tr;
+      const bool hl = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, cr, tmin, hi, tl);
+      const bool hr = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, cr, tmin, hi, tr);
+      if (hl && hr) {
+        const bool swap = tr < tl;
+        if (!push(swap ? m.x : m.y)) return false;
+        item = swap ? m.y : m.x;
+      } else if (hl) {
+        item = m.x;
+      } else if (hr) {
+        item = m.y;
+      } else {
+        item = pop();
+      }
+      if (item != ITEM_NONE && (item >> ITEM_SHIFT) != ITEM_NODE && lf == ITEM_NONE) postpone();
+      if (!__any(lf == ITEM_NONE)) break;   // every lane holds a postponed item
+    }
+    // ---------------- phase 2: leaves, instance entry / exit
+    while (lf != ITEM_NONE) {
+      const uint32_t tag = lf >> ITEM_SHIFT, idx = lf & ITEM_MASK;
+      if (tag == ITEM_LEAF) {
+        const DLeaf leaf = sc.leaves[idx];
+        const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
+        const bool world = cur_inst < 0;
+        for (int k = 0; k < n; ++k) {
+          int pk = kind;
+          uint32_t pi = leaf.first + k;
+          const int pos = int(leaf.first) + k;
+          if (kind == PK_MIXED) { const uint32_t r = sc.refs[pi]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
+          float t;
+          bool ok = false;
+          if (pk == PK_TRI) {
+            if (kCount) cnt.tri++;
+            ok = tri_t(sc.tris[pi], cr.o, cr.d, tmin, t) && (kAny ? t <= tmax : true);
+          } else if (pk == PK_QUAD) {
+            if (kCount) cnt.quad++;
+            ok = quad_t(sc.quads[pi], cr.o, cr.d, tmin, t) && (kAny ? t <= tmax : true);
+          } else if (pk == PK_SPHERE) {
+            if (kCount) cnt.sph++;
+            ok = sphere_t(sc.spheres[pi], cr.o, cr.d, time, tmin, t) && (kAny ? t < tmax : true);
+          } else if (pk == PK_INSTANCE) {
+            if (!push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos))) return false;
+            continue;
+          } else if (kVol && pk == PK_VOLUME) {
+            ok = volume_hit<kCount>(sc, sc.volumes[pi], wo, wd, time, tmin, kAny ? tmax : best.t,
+                                    leaf_ntests(leaf.info), key, bounce, voldom, t, cnt);
+          }
+          if (!ok) continue;
+          if (kAny) return true;
+          const int refpos = world ? pos : cur_ref;
+          const int primpos = world ? 0 : pos;
+          if (accept(sc, t, pk, refpos, primpos, best)) {
+            best.t = t; best.kind = pk; best.idx = int(pi); best.inst = cur_inst;
+            best.refpos = refpos; best.primpos = primpos;
+          }
+        }
+      } else if (tag == ITEM_INSTANCE) {
+        const uint32_t r = sc.refs[idx];
+        const int ii = int(r & REF_MASK);
+        const DInstance& in = sc.instances[ii];
+        if (kCount) cnt.inst++;
+        V3 o = wo, d = wd;
+        to_object(in, o, d);
+        const TRay orr = make_tray(o, d);
+        const DBvh& bb = sc.blas[in.blas];
+        bool enter = true;
+        if (bb.check_box)
+          enter = box_hit(bb.box[0], bb.box[1], bb.box[2], bb.box[3], bb.box[4], bb.box[5], orr, tmin,
+                          kAny ? tmax : best.t, tn);
+        if (enter) {
+          if (item < ITEM_POP && !push(item)) return false;
+          if (!push(ITEM_INST_END << ITEM_SHIFT)) return false;
+          cr = orr; cur_inst = ii; cur_ref = int(idx);
+          item = bb.root_item;
+        }
+      } else {  // ITEM_INST_END: back to the world-space ray
+        cr = make_tray(wo, wd); cur_inst = -1; cur_ref = -1;
+      }
+      lf = ITEM_NONE;
+      // ITEM_NONE here only means the stack was empty when this lane last
+      // popped; the leaf just processed may have pushed instance items since.
+      if (item == ITEM_POP || item == ITEM_NONE) item = pop();
+      if (item != ITEM_NONE && (item >> ITEM_SHIFT) != ITEM_NODE) postpone();
+    }
+  }
+  return kAny ? false : best.kind != 0;
+}
+
+// ----------------------------------------------------------------------------
+// Hit record for the winner (HitRecord, hittable.go:4-12; SetFaceNormal :20-30)
+// ----------------------------------------------------------------------------
+struct Rec {
+  V3 P, N;
+  bool front;
+  int mat;
+};
+
+__device__ __forceinline__ void set_face(V3 d, V3 outward, Rec& rec) {
+  rec.front = dot(d, outward) < 0.0f;
+  rec.N = rec.front ? outward : neg(outward);
+}
+
+__device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float time) {
+  Rec rec;
+  if (b.kind == PK_PLANE) {
+    const DPlane& p = sc.planes[b.idx];
+    rec.P = add(wo, scale(wd, b.t));
+    set_face(wd, mk(p.nx, p.ny, p.nz), rec);
+    rec.mat = p.mat;
+    return rec;
+  }
+  if (b.kind == PK_VOLUME) {                       // volume.go:72-76
+    const DVolume& v = sc.volumes[b.idx];
+    rec.P = add(wo, scale(wd, b.t));
+    rec.N = mk(1.0f, 0.0f, 0.0f);
+    rec.front = true;
+    rec.mat = v.mat;
+    return rec;
+  }
+  V3 o = wo, d = wd;
+  const DInstance* in = nullptr;
+  if (b.inst >= 0) { in = &sc.instances[b.inst]; to_object(*in, o, d); }
+  rec.P = add(o, scale(d, b.t));
+  if (b.kind == PK_SPHERE) {
+    const DSphere& s = sc.spheres[b.idx];
+    V3 c = add(mk(s.cx, s.cy, s.cz), scale(mk(s.vx, s.vy, s.vz), time));
+    set_face(d, divs(sub(rec.P, c), s.r), rec);
+    rec.mat = s.mat;
+  } else if (b.kind == PK_QUAD) {
+    const DQuad& q = sc.quads[b.idx];
+    set_face(d, mk(q.nx, q.ny, q.nz), rec);
+    rec.mat = q.mat;
+  } else {  // PK_TRI
+    const DTriAux& ax = sc.tri_aux[b.idx];
+    set_face(d, mk(ax.nx, ax.ny, ax.nz), rec);
+    rec.mat = ax.mat;
+  }
+  if (in) {
+    for (int i = in->nwrap - 1; i >= 0; --i) unwrap_hit(in->kind[i], in->prm[i], rec.P, rec.N);
+  }
+  return rec;
+}
+
+// ----------------------------------------------------------------------------
+// Textures / materials
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ V3 tex_value(const DScene& sc, int ti, V3 p) {
+  const DTexture& t = sc.textures[ti];
+  if (t.kind == 2) {                                   // texture.go:47-65
+    const float eps = 1e-4f;
+    int xi = int(floorf(t.inv_scale * p.x + eps));
+    int yi = int(floorf(t.inv_scale * p.y + eps));
+    int zi = int(floorf(t.inv_scale * p.z + eps));
+    bool even = ((xi + yi + zi) % 2) == 0;
+    return even ? ld3(t.even) : ld3(t.odd);
+  }
+  return ld3(t.even);
+}
+
+__device__ __forceinline__ float pow5(float x) { float x2 = x * x; return (x2 * x2) * x; }
+
+// ----------------------------------------------------------------------------
+// HDRI (hdri.go)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ V3 texel(const DEnv& e, int x, int y) {
+  const float4 v = reinterpret_cast<const float4*>(e.texels)[y * e.width + x];
+  return mk(v.x, v.y, v.z);
+}
+__device__ __forceinline__ int iclamp(int x, int lo, int hi) {   // image_loader.go:112-120
+  if (x < lo) return lo;
+  if (x < hi) return x;
+  return hi - 1;
+}
+__device__ __forceinline__ void dir_to_uv(const DEnv& e, V3 dir, float& u, float& v) {   // hdri.go:75-94
+  V3 d = unit(dir);
+  float phi = atan2f(d.z, d.x);
+  float dy = d.y > 1.0f ? 1.0f : (d.y < -1.0f ? -1.0f : d.y);
+  float theta = asinf(dy);
+  u = 0.5f + phi / (2.0f * kPi);
+  v = 0.5f - theta / kPi;
+  u = u + e.rotation / (2.0f * kPi);
+  u = u - floorf(u);
+}
+__device__ V3 env_sample(const DEnv& e, V3 dir) {          // hdri.go:120-128 + bilinear
+  float u, v;
+  dir_to_uv(e, dir, u, v);
+  float px = u * float(e.width) - 0.5f;
+  float py = v * float(e.height) - 0.5f;
+  int x0 = int(floorf(px)), y0 = int(floorf(py));
+  int x1 = x0 + 1, y1 = y0 + 1;
+  float fx = px - float(x0), fy = py - float(y0);
+  x0 = ((x0 % e.width) + e.width) % e.width;
+  x1 = ((x1 % e.width) + e.width) % e.width;
+  y0 = iclamp(y0, 0, e.height);
+  y1 = iclamp(y1, 0, e.height);
+  V3 c00 = texel(e, x0, y0), c10 = texel(e, x1, y0), c01 = texel(e, x0, y1), c11 = texel(e, x1, y1);
+  V3 c0 = add(scale(c00, 1.0f - fx), scale(c10, fx));
+  V3 c1 = add(scale(c01, 1.0f - fx), scale(c11, fx));
+  return add(scale(c0, 1.0f - fy), scale(c1, fy));
+}
+__device__ __forceinline__ int search_cdf(const float* cdf, int n, float xi) {   // hdri.go:300-322
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) / 2;
+    if (cdf[mid + 1] <= xi) lo = mid + 1; else hi = mid;
+  }
+  if (lo >= n) lo = n - 1;
+  if (lo < 0) lo = 0;
+  return lo;
+}
+__device__ float env_pdf(const DEnv& e, V3 dir) {          // hdri.go:262-297
+  float u, v;
+  dir_to_uv(e, dir, u, v);
+  int x = int(u * float(e.width)), y = int(v * float(e.height));
+  x = iclamp(x, 0, e.width);
+  y = iclamp(y, 0, e.height);
+  float theta = (0.5f - v) * kPi;
+  float st = cosf(theta);
+  if (st < 1e-10f) st = 1e-10f;
+  float p = e.pdf[y * e.width + x] * float(e.width * e.height) / (2.0f * kPi * kPi * st);
+  if (p < 1e-10f) return 1e-10f;
+  return p;
+}
+
+// ----------------------------------------------------------------------------
+// One camera sample (RayColor camera.go:438-518, iterative throughput form)
+// ----------------------------------------------------------------------------
+template <bool kCount>
+__device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, uint32_t key, int depth,
+                         uint32_t* stk, int stride, int cap, Cnt& cnt, int* err) {
+  // GetRay camera.go:368-388
+  float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
+  float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
+  float time = rnd(key, ctr(0, DOM_CAMERA, 2));
+  V3 ps = add(add(ld3(cam.pixel00), scale(ld3(cam.du), float(px) + offx)), scale(ld3(cam.dv), float(py) + offy));
+  V3 ro = ld3(cam.center);
+  if (cam.defocus) {                       // defocusDiskSample camera.go:354-362
+    V3 p = mk(0.0f, 0.0f, 0.0f);
+    for (int k = 0; k < MAX_DISK_TRIES; ++k) {
+      uint32_t c = ctr(0, DOM_CAMERA, 3u + 2u * k);
+      float x = -1.0f + 2.0f * rnd(key, c), y = -1.0f + 2.0f * rnd(key, c + 1u);
+      if (x * x + y * y + 0.0f * 0.0f < 1.0f) { p = mk(x, y, 0.0f); break; }
+    }
+    ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
+  }
+  V3 rd = sub(ps, ro);
+
+  V3 L = mk(0.0f, 0.0f, 0.0f), beta = mk(1.0f, 1.0f, 1.0f);
+  bool allow = true;
+  uint32_t bounce = 0;
+  for (int dleft = depth; dleft > 0; --dleft, ++bounce) {
+    Best b;
+    if (kCount) cnt.rays++;
+    bool hit = traverse<false, kCount>(sc, ro, rd, time, 0.001f, __builtin_inff(), stk, stride, cap, b, key,
+                                       bounce, DOM_VOL, cnt, err);
+    if (!hit) {                                               // camera.go:451-466
+      V3 bg;
+      if (sc.env.valid) {
+        if (cam.phantom && dleft == cam.cam_max_depth) bg = mk(0.0f, 0.0f, 0.0f);
+        else { bg = env_sample(sc.env, rd); if (kCount) cnt.env++; }
+      } else if (cam.use_sky) {
+        V3 ud = unit(rd);
+        float a = 0.5f * (ud.y + 1.0f);
+        bg = add(scale(mk(1.0f, 1.0f, 1.0f), 1.0f - a), scale(mk(0.5f, 0.7f, 1.0f), a));
+      } else {
+        bg = ld3(cam.background);
+      }
+      L = add(L, mul(beta, bg));
+      break;
+    }
+    Rec rec = make_record(sc, b, ro, rd, time);
+    const DMaterial& m = sc.materials[rec.mat];
+    if (kCount) cnt.mat++;
+    V3 att, sd;
+    bool use_mis = false;
+    if (m.kind == 4) {                                        // DiffuseLight: no scatter
+      if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.P)));
+      break;
+    } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
+      sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
+      if (near_zero(sd)) sd = rec.N;
+      att = tex_value(sc, m.tex, rec.P);
+      use_mis = sc.num_lights > 0;
+    } else if (m.kind == 2) {                                 // Metal material.go:113-119
+      V3 refl = reflect(rd, rec.N);
+      refl = add(unit(refl), scale(random_unit_vector(key, bounce, DOM_SCATTER, 0), m.fuzz));
+      sd = refl;
+      att = ld3(m.albedo);
+      if (!(dot(sd, rec.N) > 0.0f)) break;                    // absorbed: Emitted = 0
+    } else if (m.kind == 3) {                                 // Dielectric material.go:164-188
+      att = mk(1.0f, 1.0f, 1.0f);
+      float ri = rec.front ? (1.0f / m.ior) : m.ior;
+      V3 ud = unit(rd);
+      float c = dot(neg(ud), rec.N);
+      float ct = c < 1.0f ? c : 1.0f;
+      float st = sqrtf(1.0f - ct * ct);
+      bool cannot = ri * st > 1.0f;
+      bool refl = cannot;
+      if (!cannot) {
+        float r0 = (1.0f - ri) / (1.0f + ri);
+        r0 = r0 * r0;
+        float rf = r0 + (1.0f - r0) * pow5(1.0f - ct);
+        refl = rf > rnd(key, ctr(bounce, DOM_FRESNEL, 0));
+      }
+      sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
+    } else {                                                  // Isotropic material.go:266-270
+      sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
+      att = tex_value(sc, m.tex, rec.P);
+    }
+    if (use_mis) {                                            // camera.go:502-517
+      int nl = sc.num_lights;
+      int li = int(rnd(key, ctr(bounce, DOM_NEE, 0)) * float(nl));
+      if (li >= nl) li = nl - 1;
+      V3 direct = mk(0.0f, 0.0f, 0.0f);
+      if (sc.env.valid && sc.env.use_is) {                    // sampleHDRILight camera.go:565-607
+        const DEnv& e = sc.env;
+        V3 ldir, em;
+        float pdfH;
+        if (!(e.total_power > 0.0f)) {
+          ldir = random_unit_vector(key, bounce, DOM_NEE, 5);
+          em = env_sample(e, ldir);
+          pdfH = 1.0f / (4.0f * kPi);
+        } else {
+          float xi1 = rnd(key, ctr(bounce, DOM_NEE, 3));
+          int y = search_cdf(e.marginal, e.height, xi1);
+          float xi2 = rnd(key, ctr(bounce, DOM_NEE, 4));
+          int x = search_cdf(e.conditional + size_t(y) * (e.width + 1), e.width, xi2);
+          float uu = (float(x) + 0.5f) / float(e.width);
+          float vv = (float(y) + 0.5f) / float(e.height);
+          uu = uu - e.rotation / (2.0f * kPi);               // UVToDirection hdri.go:97-113
+          uu = uu - floorf(uu);
+          float phi = (uu - 0.5f) * 2.0f * kPi;
+          float th = (0.5f - vv) * kPi;
+          float ctt = cosf(th);
+          ldir = mk(ctt * cosf(phi), sinf(th), ctt * sinf(phi));
+          em = texel(e, x, y);
+          pdfH = env_pdf(e, ldir);
+        }
+        float cth = dot(rec.N, ldir);
+        if (cth > 0.0f) {
+          Best sb;
+          if (kCount) cnt.shadow++;
+          bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, __builtin_inff(), stk, stride, cap,
+                                                sb, key, bounce, DOM_VOL_SH_HDRI, cnt, err);
+          if (!blocked) {
+            float c2 = dot(rec.N, ldir);
+            float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
+            float w = pdfH / (pdfH + pdfB);
+            V3 ct = mul(scale(em, cth / pdfH * w), att);
+            direct = add(direct, mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f)));
+          }
+        }
+      }
+      if (li < nl) {                                          // sampleAreaLight camera.go:610-678
+        const DLight& lt = sc.lights[li];
+        if (lt.is_quad) {
+          float al = rnd(key, ctr(bounce, DOM_NEE, 1)), be = rnd(key, ctr(bounce, DOM_NEE, 2));
+          V3 lp = add(add(ld3(lt.Q), scale(ld3(lt.u), al)), scale(ld3(lt.v), be));
+          V3 tl = sub(lp, rec.P);
+          float dist = len(tl);
+          V3 ldir = unit(tl);
+          float cth = dot(rec.N, ldir);
+          if (cth > 0.0f) {
+            Best sb;
+            if (kCount) cnt.shadow++;
+            bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, dist - 0.001f, stk, stride, cap,
+                                                  sb, key, bounce, DOM_VOL_SH_AREA, cnt, err);
+            if (!blocked) {
+              const DMaterial& lm = sc.materials[lt.mat];
+              V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, lp) : mk(0.0f, 0.0f, 0.0f);
+              float area = len(cross(ld3(lt.u), ld3(lt.v)));
+              float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
+              if (!(cl < 0.001f)) {
+                float pdfL = (dist * dist) / (cl * area);
+                float c2 = dot(rec.N, ldir);
+                float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
+                float w = pdfL / (pdfL + pdfB);
+                V3 ct = scale(mul(scale(em, cth / pdfL * w), att), float(nl));
+                direct = add(direct, mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f)));
+              }
+            }
+          }
+        }
+      }
+      L = add(L, mul(beta, direct));
+      allow = false;
+    } else {
+      allow = true;
+    }
+    beta = mul(beta, att);
+    ro = rec.P;
+    rd = sd;
+  }
+  return L;
+}
+
+}  // namespace rtg

@@ -214,6 +214,11 @@ int rt_render(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* pa
 int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                      float* accum_rgb_device, void* hip_stream);
 
+/* Device time (ms) of the render kernel of the most recent render call on
+ * this context (hipEvents recorded on that call's stream around the render
+ * kernel only); blocks until that kernel has finished.                    */
+int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms);
+
 /* Instrumented run of the same kernel: traversal/prim counters. */
 int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                   rt_work_counts* out);
