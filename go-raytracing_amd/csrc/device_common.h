@@ -361,136 +361,178 @@ __device__ bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, f
 constexpr uint32_t ITEM_NONE = 0xFFFFFFFFu;
 constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the stack"
 
-template <bool kAny, bool kCount, bool kVol = true>
-__device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin, float tmax,
-                         uint32_t* stk, int stride, int cap, Best& best, uint32_t key,
-                         uint32_t bounce, uint32_t voldom, Cnt& cnt, int* err) {
+// Resumable traversal state (one lane, one ray).
+struct Trav {
+  V3 wo, wd;             // world-space ray (instances / volumes / restore)
+  TRay cr;               // current-space ray (object space inside an instance)
+  float time, tmin, tmax;
+  uint32_t key, bounce, voldom;
+  uint32_t item, lf;
+  int sp, cur_inst, cur_ref;
+  Best best;
+};
+
+enum : int { TRAV_RUNNING = 0, TRAV_DONE = 1, TRAV_ANYHIT = 2 };
+
+// Set up one ray: planes (lifted out of the BVH) and the root box.
+template <bool kAny, bool kCount>
+__device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, V3 wo, V3 wd, float time, float tmin, float tmax,
+                                         uint32_t key, uint32_t bounce, uint32_t voldom, Cnt& cnt) {
+  T.wo = wo; T.wd = wd; T.time = time; T.tmin = tmin; T.tmax = tmax;
+  T.key = key; T.bounce = bounce; T.voldom = voldom;
+  Best& best = T.best;
   best.t = tmax; best.kind = 0; best.idx = -1; best.inst = -1; best.refpos = 0; best.primpos = 0;
-  // Planes (pulled out of the BVH: universe bbox).
   for (int i = 0; i < sc.num_planes; ++i) {
     float t;
     if (kCount) cnt.plane++;
     if (plane_t(sc.planes[i], wo, wd, tmin, t)) {
-      if (kAny) { if (t < tmax) return true; }
+      if (kAny) { if (t < tmax) return TRAV_ANYHIT; }
       else if (accept(sc, t, PK_PLANE, -1 - i, 0, best)) {
         best.t = t; best.kind = PK_PLANE; best.idx = i; best.inst = -1; best.refpos = -1 - i; best.primpos = 0;
       }
     }
   }
-  TRay cr = make_tray(wo, wd);
-  int cur_inst = -1, cur_ref = -1;
+  T.cr = make_tray(wo, wd);
+  T.cur_inst = -1; T.cur_ref = -1; T.sp = 0;
+  T.item = ITEM_NONE; T.lf = ITEM_NONE;
   float tn;
   if (sc.tlas.check_box &&
       !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
-               cr, tmin, kAny ? tmax : best.t, tn))
-    return kAny ? false : best.kind != 0;
-  int sp = 0;
-  uint32_t item = sc.tlas.root_item, lf = ITEM_NONE;
-  auto pop = [&]() -> uint32_t { if (sp == 0) return ITEM_NONE; --sp; return stk[sp * stride]; };
-  auto push = [&](uint32_t v) -> bool {
-    if (sp >= cap) { *err = 1; return false; }
-    stk[sp * stride] = v; ++sp; return true;
-  };
-  // park a non-node item in lf (leaves allow speculative traversal to go on)
-  auto postpone = [&]() {
-    lf = item;
-    item = ((lf >> ITEM_SHIFT) == ITEM_LEAF) ? pop() : ITEM_POP;
-  };
-  if ((item >> ITEM_SHIFT) != ITEM_NODE) postpone();
-  while (item != ITEM_NONE || lf != ITEM_NONE) {
-    // ---------------- phase 1: internal nodes
-    while (item < ITEM_POP && (item >> ITEM_SHIFT) == ITEM_NODE) {
-      const float4* np = reinterpret_cast<const float4*>(sc.nodes + (item & ITEM_MASK));
-      const float4 a = np[0], b = np[1], c = np[2];
-      const uint4 m = reinterpret_cast<const uint4*>(np)[3];
-      if (kCount) cnt.nodes++;
-      const float hi = kAny ? tmax : best.t;
-      float tl, tr;
-      const bool hl = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, cr, tmin, hi, tl);
-      const bool hr = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, cr, tmin, hi, tr);
-      if (hl && hr) {
-        const bool swap = tr < tl;
-        if (!push(swap ? m.x : m.y)) return false;
-        item = swap ? m.y : m.x;
-      } else if (hl) {
-        item = m.x;
-      } else if (hr) {
-        item = m.y;
-      } else {
-        item = pop();
-      }
-      if (item != ITEM_NONE && (item >> ITEM_SHIFT) != ITEM_NODE && lf == ITEM_NONE) postpone();
-      if (!__any(lf == ITEM_NONE)) break;   // every lane holds a postponed item
-    }
-    // ---------------- phase 2: leaves, instance entry / exit
-    while (lf != ITEM_NONE) {
-      const uint32_t tag = lf >> ITEM_SHIFT, idx = lf & ITEM_MASK;
-      if (tag == ITEM_LEAF) {
-        const DLeaf leaf = sc.leaves[idx];
-        const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
-        const bool world = cur_inst < 0;
-        for (int k = 0; k < n; ++k) {
-          int pk = kind;
-          uint32_t pi = leaf.first + k;
-          const int pos = int(leaf.first) + k;
-          if (kind == PK_MIXED) { const uint32_t r = sc.refs[pi]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
-          float t;
-          bool ok = false;
-          if (pk == PK_TRI) {
-            if (kCount) cnt.tri++;
-            ok = tri_t(sc.tris[pi], cr.o, cr.d, tmin, t) && (kAny ? t <= tmax : true);
-          } else if (pk == PK_QUAD) {
-            if (kCount) cnt.quad++;
-            ok = quad_t(sc.quads[pi], cr.o, cr.d, tmin, t) && (kAny ? t <= tmax : true);
-          } else if (pk == PK_SPHERE) {
-            if (kCount) cnt.sph++;
-            ok = sphere_t(sc.spheres[pi], cr.o, cr.d, time, tmin, t) && (kAny ? t < tmax : true);
-          } else if (pk == PK_INSTANCE) {
-            if (!push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos))) return false;
-            continue;
-          } else if (kVol && pk == PK_VOLUME) {
-            ok = volume_hit<kCount>(sc, sc.volumes[pi], wo, wd, time, tmin, kAny ? tmax : best.t,
-                                    leaf_ntests(leaf.info), key, bounce, voldom, t, cnt);
-          }
-          if (!ok) continue;
-          if (kAny) return true;
-          const int refpos = world ? pos : cur_ref;
-          const int primpos = world ? 0 : pos;
-          if (accept(sc, t, pk, refpos, primpos, best)) {
-            best.t = t; best.kind = pk; best.idx = int(pi); best.inst = cur_inst;
-            best.refpos = refpos; best.primpos = primpos;
-          }
-        }
-      } else if (tag == ITEM_INSTANCE) {
-        const uint32_t r = sc.refs[idx];
-        const int ii = int(r & REF_MASK);
-        const DInstance& in = sc.instances[ii];
-        if (kCount) cnt.inst++;
-        V3 o = wo, d = wd;
-        to_object(in, o, d);
-        const TRay orr = make_tray(o, d);
-        const DBvh& bb = sc.blas[in.blas];
-        bool enter = true;
-        if (bb.check_box)
-          enter = box_hit(bb.box[0], bb.box[1], bb.box[2], bb.box[3], bb.box[4], bb.box[5], orr, tmin,
-                          kAny ? tmax : best.t, tn);
-        if (enter) {
-          if (item < ITEM_POP && !push(item)) return false;
-          if (!push(ITEM_INST_END << ITEM_SHIFT)) return false;
-          cr = orr; cur_inst = ii; cur_ref = int(idx);
-          item = bb.root_item;
-        }
-      } else {  // ITEM_INST_END: back to the world-space ray
-        cr = make_tray(wo, wd); cur_inst = -1; cur_ref = -1;
-      }
-      lf = ITEM_NONE;
-      // ITEM_NONE here only means the stack was empty when this lane last
-      // popped; the leaf just processed may have pushed instance items since.
-      if (item == ITEM_POP || item == ITEM_NONE) item = pop();
-      if (item != ITEM_NONE && (item >> ITEM_SHIFT) != ITEM_NODE) postpone();
-    }
+               T.cr, tmin, kAny ? tmax : best.t, tn))
+    return TRAV_DONE;
+  T.item = sc.tlas.root_item;
+  if ((T.item >> ITEM_SHIFT) != ITEM_NODE) {
+    T.lf = T.item;
+    T.item = ((T.lf >> ITEM_SHIFT) == ITEM_LEAF) ? ITEM_NONE : ITEM_POP;
   }
-  return kAny ? false : best.kind != 0;
+  return TRAV_RUNNING;
+}
+
+// One "while-while" round (Aila & Laine 2009, wave64): phase 1 walks internal
+// nodes until every lane of the wave holds a postponed leaf / instance
+// item (ballot), phase 2 processes those.  Closest hit with the DFS tie rule,
+// independent of visiting order (BVHNode.Hit bvh.go:219-239 is left-first).
+//   kAny = false: closest hit in [tmin, tmax) with the tie rule.
+//   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
+template <bool kAny, bool kCount, bool kVol>
+__device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* stk, int stride, int cap, Cnt& cnt,
+                                         int* err) {
+  Best& best = T.best;
+  auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return stk[T.sp * stride]; };
+  auto push = [&](uint32_t v) -> bool {
+    if (T.sp >= cap) { *err = 1; return false; }
+    stk[T.sp * stride] = v; ++T.sp; return true;
+  };
+  auto postpone = [&]() {
+    T.lf = T.item;
+    T.item = ((T.lf >> ITEM_SHIFT) == ITEM_LEAF) ? pop() : ITEM_POP;
+  };
+  // ---------------- phase 1: internal nodes
+  while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
+    const float4* np = reinterpret_cast<const float4*>(sc.nodes + (T.item & ITEM_MASK));
+    const float4 a = np[0], b = np[1], c = np[2];
+    const uint4 m = reinterpret_cast<const uint4*>(np)[3];
+    if (kCount) cnt.nodes++;
+    const float hi = kAny ? T.tmax : best.t;
+    float tl, tr;
+    const bool hl = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, T.cr, T.tmin, hi, tl);
+    const bool hr = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, T.cr, T.tmin, hi, tr);
+    if (hl && hr) {
+      const bool swap = tr < tl;
+      if (!push(swap ? m.x : m.y)) return TRAV_DONE;
+      T.item = swap ? m.y : m.x;
+    } else if (hl) {
+      T.item = m.x;
+    } else if (hr) {
+      T.item = m.y;
+    } else {
+      T.item = pop();
+    }
+    if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
+    if (!__any(T.lf == ITEM_NONE)) break;   // every lane holds a postponed item
+  }
+  // ---------------- phase 2: leaves, instance entry / exit
+  while (T.lf != ITEM_NONE) {
+    const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
+    if (tag == ITEM_LEAF) {
+      const DLeaf leaf = sc.leaves[idx];
+      const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
+      const bool world = T.cur_inst < 0;
+      for (int k = 0; k < n; ++k) {
+        int pk = kind;
+        uint32_t pi = leaf.first + k;
+        const int pos = int(leaf.first) + k;
+        if (kind == PK_MIXED) { const uint32_t r = sc.refs[pi]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
+        float t;
+        bool ok = false;
+        if (pk == PK_TRI) {
+          if (kCount) cnt.tri++;
+          ok = tri_t(sc.tris[pi], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
+        } else if (pk == PK_QUAD) {
+          if (kCount) cnt.quad++;
+          ok = quad_t(sc.quads[pi], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
+        } else if (pk == PK_SPHERE) {
+          if (kCount) cnt.sph++;
+          ok = sphere_t(sc.spheres[pi], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+        } else if (pk == PK_INSTANCE) {
+          if (!push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos))) return TRAV_DONE;
+          continue;
+        } else if (kVol && pk == PK_VOLUME) {
+          ok = volume_hit<kCount>(sc, sc.volumes[pi], T.wo, T.wd, T.time, T.tmin, kAny ? T.tmax : best.t,
+                                  leaf_ntests(leaf.info), T.key, T.bounce, T.voldom, t, cnt);
+        }
+        if (!ok) continue;
+        if (kAny) return TRAV_ANYHIT;
+        const int refpos = world ? pos : T.cur_ref;
+        const int primpos = world ? 0 : pos;
+        if (accept(sc, t, pk, refpos, primpos, best)) {
+          best.t = t; best.kind = pk; best.idx = int(pi); best.inst = T.cur_inst;
+          best.refpos = refpos; best.primpos = primpos;
+        }
+      }
+    } else if (tag == ITEM_INSTANCE) {
+      const uint32_t r = sc.refs[idx];
+      const int ii = int(r & REF_MASK);
+      const DInstance& in = sc.instances[ii];
+      if (kCount) cnt.inst++;
+      V3 o = T.wo, d = T.wd;
+      to_object(in, o, d);
+      const TRay orr = make_tray(o, d);
+      const DBvh& bb = sc.blas[in.blas];
+      bool enter = true;
+      float tn;
+      if (bb.check_box)
+        enter = box_hit(bb.box[0], bb.box[1], bb.box[2], bb.box[3], bb.box[4], bb.box[5], orr, T.tmin,
+                        kAny ? T.tmax : best.t, tn);
+      if (enter) {
+        if (T.item < ITEM_POP && !push(T.item)) return TRAV_DONE;
+        if (!push(ITEM_INST_END << ITEM_SHIFT)) return TRAV_DONE;
+        T.cr = orr; T.cur_inst = ii; T.cur_ref = int(idx);
+        T.item = bb.root_item;
+      }
+    } else {  // ITEM_INST_END: back to the world-space ray
+      T.cr = make_tray(T.wo, T.wd); T.cur_inst = -1; T.cur_ref = -1;
+    }
+    T.lf = ITEM_NONE;
+    // ITEM_NONE here only means the stack was empty when this lane last
+    // popped; the leaf just processed may have pushed instance items since.
+    if (T.item == ITEM_POP || T.item == ITEM_NONE) T.item = pop();
+    if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE) postpone();
+  }
+  return (T.item == ITEM_NONE && T.lf == ITEM_NONE) ? TRAV_DONE : TRAV_RUNNING;
+}
+
+// Whole-ray traversal (probe kernel, megakernel).
+template <bool kAny, bool kCount, bool kVol = true>
+__device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin, float tmax,
+                         uint32_t* stk, int stride, int cap, Best& best, uint32_t key,
+                         uint32_t bounce, uint32_t voldom, Cnt& cnt, int* err) {
+  Trav T;
+  int s = trav_init<kAny, kCount>(sc, T, wo, wd, time, tmin, tmax, key, bounce, voldom, cnt);
+  while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol>(sc, T, stk, stride, cap, cnt, err);
+  best = T.best;
+  if (kAny) return s == TRAV_ANYHIT;
+  return best.kind != 0;
 }
 
 // ----------------------------------------------------------------------------

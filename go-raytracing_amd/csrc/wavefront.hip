@@ -96,26 +96,76 @@ __global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, uint32_
   }
 }
 
+// ---------------------------------------------------------------- refill
+// Persistent traversal lanes: when at least kRefill lanes of a wave are idle,
+// the wave grabs that many queue entries with one atomic (ballot + mbcnt).
+constexpr int kRefill = 16;
+
+struct Fetch {
+  uint32_t idx;      // queue index for this lane (valid if < n)
+  bool exhausted;    // wave-uniform: the queue is drained
+};
+__device__ __forceinline__ Fetch wave_fetch(bool idle, uint32_t* ctr, uint32_t n) {
+  Fetch f{0xFFFFFFFFu, false};
+  const unsigned long long m = __ballot(idle);
+  const int nidle = __popcll(m);
+  if (nidle < kRefill) return f;
+  const int lane = __lane_id();
+  const int leader = __ffsll(m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, uint32_t(nidle));
+  base = __shfl(base, leader);
+  f.exhausted = base + uint32_t(nidle) >= n;
+  if (idle) f.idx = base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+  return f;
+}
+
 // ---------------------------------------------------------------- extend
 template <int STACK, bool kCount, bool kVol>
 __global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uint32_t* q, const uint32_t* count,
-                                                uint32_t* zero_a, uint32_t* zero_b) {
+                                                uint32_t* zero_a, uint32_t* zero_b, uint32_t* fetch,
+                                                uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[STACK * 256];
-  if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; }   // next queues
+  if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
   const uint32_t n = *count;
-  const uint32_t gs = gridDim.x * blockDim.x;
+  uint32_t* stk = lds_stack + threadIdx.x;
   Cnt cnt = {};
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-    const uint32_t p = q[i];
-    const float4 o = a.ray_o[p], d = a.ray_d[p];
-    uint32_t bounce = 0;
-    if (kVol) bounce = (asu(a.beta[p].w) >> 16) & 0x7FFFu;
-    Best b;
-    if (kCount) cnt.rays++;
-    bool hit = traverse<false, kCount, kVol>(sc, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, 0.001f, __builtin_inff(),
-                                       lds_stack + threadIdx.x, 256, STACK, b, asu(d.w), bounce, DOM_VOL, cnt, a.err);
-    a.hit[p] = make_float4(b.t, asf(hit ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
-                           0.0f);
+  Trav T;
+  uint32_t p = ITEM_NONE;
+  bool exhausted = false;
+  for (;;) {
+    if (!exhausted) {
+      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n);
+      exhausted = f.exhausted;
+      if (f.idx < n) {
+        p = q[f.idx];
+        const float4 o = a.ray_o[p], d = a.ray_d[p];
+        uint32_t bounce = 0;
+        if (kVol) bounce = (asu(a.beta[p].w) >> 16) & 0x7FFFu;
+        if (kCount) cnt.rays++;
+        const int s = trav_init<false, kCount>(sc, T, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, 0.001f,
+                                               __builtin_inff(), asu(d.w), bounce, DOM_VOL, cnt);
+        if (s != TRAV_RUNNING) {
+          const Best& b = T.best;
+          a.hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u),
+                                 asf(uint32_t(b.inst)), 0.0f);
+          p = ITEM_NONE;
+        }
+      }
+    }
+    if (!__any(p != ITEM_NONE)) {
+      if (exhausted) break;
+      continue;
+    }
+    if (p != ITEM_NONE) {
+      const int s = trav_step<false, kCount, kVol>(sc, T, stk, 256, STACK, cnt, a.err);
+      if (s != TRAV_RUNNING) {
+        const Best& b = T.best;
+        a.hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u),
+                               asf(uint32_t(b.inst)), 0.0f);
+        p = ITEM_NONE;
+      }
+    }
   }
   if (kCount) add_counters(a.counters, cnt, 0);
 }
@@ -302,39 +352,72 @@ __global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs 
 }
 
 // ---------------------------------------------------------------- shadow
+// One job = one path's NEE: HDRI ray (flag 2) then area-light ray (flag 1);
+// the visible contributions are summed in that order (camera.go:549-558) and
+// added once: L += beta_at_bounce * direct.
 template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256) void k_shadow(DScene sc, WaveArgs a) {
+__global__ __launch_bounds__(256) void k_shadow(DScene sc, WaveArgs a, uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[STACK * 256];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
   const uint32_t n = *a.shcount;
-  const uint32_t gs = gridDim.x * blockDim.x;
+  uint32_t* stk = lds_stack + threadIdx.x;
   Cnt cnt = {};
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-    const uint32_t p = a.shq[i];
-    const float4 P4 = a.sh_p[p];
-    const uint32_t f = asu(P4.w);
-    const uint32_t bounce = f >> 8;
-    const uint32_t key = asu(a.ray_d[p].w);
-    const V3 P = mk(P4.x, P4.y, P4.z);
-    V3 direct = mk(0.0f, 0.0f, 0.0f);
-    Best sb;
-    for (int r = 0; r < 2; ++r) {                                // HDRI ray first, then the area light
-      const uint32_t bit = r == 0 ? 2u : 1u;
-      if (!(f & bit)) continue;
-      const float4 dd = r == 0 ? a.sh_dh[p] : a.sh_da[p];
-      const float tmax = r == 0 ? __builtin_inff() : dd.w;     // camera.go:582 / :639
-      if (kCount) cnt.shadow++;
-      bool blocked = traverse<true, kCount, kVol>(sc, P, mk(dd.x, dd.y, dd.z), 0.0f, 0.001f, tmax, lds_stack + threadIdx.x,
-                                            256, STACK, sb, key, bounce, r == 0 ? DOM_VOL_SH_HDRI : DOM_VOL_SH_AREA,
-                                            cnt, a.err);
-      if (!blocked) {
-        const float4 c = r == 0 ? a.pend_h[p] : a.pend_a[p];
-        direct = add(direct, mk(c.x, c.y, c.z));
-      }
+  Trav T;
+  uint32_t p = ITEM_NONE, flags = 0, key = 0, bounce = 0;
+  int r = 0;
+  V3 P = mk(0.0f, 0.0f, 0.0f), direct = mk(0.0f, 0.0f, 0.0f);
+  bool exhausted = false;
+  // start ray `r` of the current job; returns the init status
+  auto start_ray = [&](int rr) -> int {
+    const float4 dd = rr == 0 ? a.sh_dh[p] : a.sh_da[p];
+    const float tmax = rr == 0 ? __builtin_inff() : dd.w;      // camera.go:582 / :639
+    if (kCount) cnt.shadow++;
+    return trav_init<true, kCount>(sc, T, P, mk(dd.x, dd.y, dd.z), 0.0f, 0.001f, tmax, key, bounce,
+                                   rr == 0 ? DOM_VOL_SH_HDRI : DOM_VOL_SH_AREA, cnt);
+  };
+  // a ray finished with status s; returns true when the whole job is done
+  auto finish_ray = [&](int s) -> bool {
+    if (s != TRAV_ANYHIT) {
+      const float4 c = r == 0 ? a.pend_h[p] : a.pend_a[p];
+      direct = add(direct, mk(c.x, c.y, c.z));
+    }
+    while (r == 0 && (flags & 1u)) {
+      r = 1;
+      const int s2 = start_ray(1);
+      if (s2 == TRAV_RUNNING) return false;
+      if (s2 != TRAV_ANYHIT) { const float4 c = a.pend_a[p]; direct = add(direct, mk(c.x, c.y, c.z)); }
     }
     const float4 pb = a.pbeta[p];
-    float4 L4 = a.L[p];
-    V3 L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
+    const float4 L4 = a.L[p];
+    const V3 L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
     a.L[p] = make_float4(L.x, L.y, L.z, L4.w);
+    return true;
+  };
+  for (;;) {
+    if (!exhausted) {
+      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n);
+      exhausted = f.exhausted;
+      if (f.idx < n) {
+        p = a.shq[f.idx];
+        const float4 P4 = a.sh_p[p];
+        flags = asu(P4.w) & 0xFFu;
+        bounce = asu(P4.w) >> 8;
+        key = asu(a.ray_d[p].w);
+        P = mk(P4.x, P4.y, P4.z);
+        direct = mk(0.0f, 0.0f, 0.0f);
+        r = (flags & 2u) ? 0 : 1;
+        const int s = start_ray(r);
+        if (s != TRAV_RUNNING && finish_ray(s)) p = ITEM_NONE;
+      }
+    }
+    if (!__any(p != ITEM_NONE)) {
+      if (exhausted) break;
+      continue;
+    }
+    if (p != ITEM_NONE) {
+      const int s = trav_step<true, kCount, kVol>(sc, T, stk, 256, STACK, cnt, a.err);
+      if (s != TRAV_RUNNING && finish_ray(s)) p = ITEM_NONE;
+    }
   }
   if (kCount) add_counters(a.counters, cnt, 0);
 }
@@ -363,7 +446,7 @@ __global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int ac
 }
 
 __global__ void k_set_counts(uint32_t* c, uint32_t n) {
-  if (threadIdx.x == 0) { c[0] = n; c[1] = 0u; c[2] = 0u; }
+  if (threadIdx.x == 0) { c[0] = n; c[1] = 0u; c[2] = 0u; c[3] = 0u; c[4] = 0u; }
 }
 
 __global__ void k_count_samples(WaveArgs a, uint32_t n) {
@@ -399,9 +482,11 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
       uint32_t* nq = (b & 1) ? a.q0 : a.q1;
       uint32_t* cc = a.counts + (b & 1);
       uint32_t* nc = a.counts + ((b & 1) ^ 1);
-      hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, cq, cc, nc, a.shcount);
+      hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, cq, cc, nc, a.shcount,
+                         a.counts + 3, a.counts + 4);
       hipLaunchKernelGGL((k_shade<kCount>), dim3(gsh), dim3(256), 0, st, sc, cam, a, cq, cc, nq, nc);
-      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol>), dim3(gsd), dim3(256), 0, st, sc, a);
+      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol>), dim3(gsd), dim3(256), 0, st, sc, a, a.counts + 4,
+                         a.counts + 3);
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
         // long-tail scenes (RandomScene depth 50): stop once every path ended
         uint32_t left = 0;
