@@ -39,11 +39,17 @@ BYTES = {
     "quad_tests": 64,
     "plane_tests": 32,
     "instance_visits": 96,   # 3x4 affine + inverse (SURVEY: 96 B)
+    "instance_box_tests": 32,  # world-space instance culling box
     "volume_tests": 64,
     "material_fetches": 32,
     "env_lookups": 48,       # 4 texels x 12 B
 }
 ACCUM_BYTES_PER_SAMPLE = 12
+# Per-ray state each wavefront kernel streams:
+# extend: queue entry 4 + ray o,d 32 + hit record 16 = 52 B per ray;
+# shadow: direction 16 + pending contribution 16 + a share of the per-path
+# origin / throughput / L read-modify-write 16 = 48 B per shadow ray.
+RAY_IO_BYTES = {"extend": 52, "shadow": 48}
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
@@ -60,7 +66,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented count run")
-    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the CPU baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=48, help="spp of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
     return ap.parse_args()
 
@@ -110,15 +116,20 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     kernel_ms = []
+    kernel_times = []
 
     def step(timed: bool):
         accum.zero_()
         ctx.render_device(cam, params, accum.data_ptr(), stream.cuda_stream)
         if timed:
             kernel_ms.append(ctx.last_render_kernel_ms())
+            kernel_times.append(ctx.last_kernel_times())
         if dist is not None:
             dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
 
+    # one HIP event before each extend/shade/shadow launch (and after each
+    # shadow launch) on the render stream: per-kernel launch durations
+    ctx.set_kernel_timing(True)
     for _ in range(args.warmup):
         step(False)
     if dist is not None:
@@ -143,22 +154,38 @@ def main():
 
     roofline = None
     work = None
+    kernels = None
     if rank == 0 and not args.no_count:
-        work = ctx.count_work(cam, params)
-        alg = sum(BYTES[k] * work[k] for k in BYTES) + ACCUM_BYTES_PER_SAMPLE * work["samples"]
-        avg_s = float(np.mean(kernel_ms)) / 1e3
-        achieved = alg / avg_s / 1e9
+        work_k = ctx.count_work_by_kernel(cam, params)
+        work = {k: sum(w[k] for w in work_k.values()) for k in work_k["extend"]}
+        kernels = {}
+        for kname in ("extend", "shade", "shadow"):
+            wk = work_k[kname]
+            alg = sum(BYTES[k] * wk[k] for k in BYTES)
+            if kname == "extend":
+                alg += RAY_IO_BYTES["extend"] * wk["rays"]
+            elif kname == "shadow":
+                alg += RAY_IO_BYTES["shadow"] * wk["shadow_rays"]
+            launches = int(np.mean([t[f"{kname}_launches"] for t in kernel_times]))
+            ms_tot = float(np.mean([t[f"{kname}_ms"] for t in kernel_times]))
+            kernels[kname] = {"launches": launches, "ms_total": round(ms_tot, 3),
+                              "ms_avg": round(ms_tot / max(launches, 1), 4),
+                              "alg_bytes_per_launch": int(alg / max(launches, 1)),
+                              "achieved_GBs": round(alg / (ms_tot / 1e3) / 1e9, 2) if ms_tot > 0 else None}
+        dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
+        kd = kernels[dom]
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}x{spp}_n{world}.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                traffic = json.load(open(pmc))["kernels"][dom]["hbm_bytes_per_launch"]
             except Exception:
                 traffic = None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "render_kernel", "kernel_ms_avg": round(avg_s * 1e3, 3),
-                    "alg_bytes_per_launch": int(alg)}
+        roofline = {"bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": f"k_{dom}", "kernel_ms_avg": kd["ms_avg"], "launches_per_step": kd["launches"],
+                    "alg_bytes_per_launch": kd["alg_bytes_per_launch"],
+                    "pipeline_ms_avg": round(float(np.mean(kernel_ms)), 3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -198,6 +225,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if kernels is not None:
+            line["kernels"] = kernels
         if work is not None:
             line["work_per_sample"] = {k: round(v / max(work["samples"], 1), 3) for k, v in work.items()
                                        if k != "samples"}

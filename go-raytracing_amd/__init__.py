@@ -93,7 +93,14 @@ class RtStats(C.Structure):
 class RtWorkCounts(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "rays", "shadow_rays", "node_visits", "sphere_tests",
                                           "quad_tests", "tri_tests", "plane_tests", "instance_visits",
-                                          "volume_tests", "material_fetches", "env_lookups")]
+                                          "volume_tests", "material_fetches", "env_lookups",
+                                          "instance_box_tests")]
+
+
+class RtKernelTimes(C.Structure):
+    _fields_ = [("extend_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double),
+                ("extend_launches", C.c_int32), ("shade_launches", C.c_int32), ("shadow_launches", C.c_int32),
+                ("pad", C.c_int32)]
 
 
 class RtSceneInfo(C.Structure):
@@ -139,6 +146,10 @@ def rtgpu() -> C.CDLL:
         lib.rt_last_render_kernel_ms.argtypes = [P, C.POINTER(C.c_double)]
         lib.rt_count_work.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
                                       C.POINTER(RtWorkCounts)]
+        lib.rt_count_work_by_kernel.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
+                                                C.POINTER(RtWorkCounts)]
+        lib.rt_set_kernel_timing.argtypes = [P, C.c_int]
+        lib.rt_last_kernel_times.argtypes = [P, C.POINTER(RtKernelTimes)]
         lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
         lib.rt_primary_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32), C.POINTER(I32),
                                         C.POINTER(C.c_float)]
@@ -355,6 +366,21 @@ class Context:
         w = RtWorkCounts()
         self._check(self._lib.rt_count_work(self._h, C.byref(camera), C.byref(params), C.byref(w)))
         return {n: int(getattr(w, n)) for n, _ in RtWorkCounts._fields_}
+
+    def count_work_by_kernel(self, camera: RtCameraDesc, params: RtRenderParams) -> dict:
+        """{"extend": counts, "shade": counts, "shadow": counts} (rt_count_work_by_kernel)."""
+        w = (RtWorkCounts * 3)()
+        self._check(self._lib.rt_count_work_by_kernel(self._h, C.byref(camera), C.byref(params), w))
+        return {k: {n: int(getattr(w[i], n)) for n, _ in RtWorkCounts._fields_}
+                for i, k in enumerate(("extend", "shade", "shadow"))}
+
+    def set_kernel_timing(self, enable: bool = True):
+        self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))
+
+    def last_kernel_times(self) -> dict:
+        t = RtKernelTimes()
+        self._check(self._lib.rt_last_kernel_times(self._h, C.byref(t)))
+        return {n: getattr(t, n) for n, _ in RtKernelTimes._fields_ if n != "pad"}
 
     def tonemap(self, accum: np.ndarray, spp: int) -> np.ndarray:
         h, w = accum.shape[:2]

@@ -51,9 +51,17 @@ struct rt_ctx {
   uint32_t* pix_pinned = nullptr;
   size_t pix_pinned_n = 0;
   hipEvent_t pix_ev = nullptr;
+  // per-launch kernel timing (rt_set_kernel_timing)
+  bool timing = false;
+  std::vector<hipEvent_t> tev;
+  std::vector<uint8_t> tev_class;
+  int tev_used = 0;
 };
 
 namespace {
+
+constexpr int CNT_WORDS = 3 * CNT_BLOCK;   // extend, shade, shadow blocks
+constexpr int MAX_TIMING_EVENTS = 1 << 16;
 
 int set_err(rt_ctx* c, int code, const std::string& m) {
   if (c) c->error = m;
@@ -188,7 +196,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   }
   if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->wacc, size_t(npix) * 3 * sizeof(double)))) return rc;
-  if ((rc = ensure(ctx, ctx->counters, 16 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ensure(ctx, ctx->counters, CNT_WORDS * sizeof(unsigned long long)))) return rc;
   if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
   // pixel list through pinned staging (async-safe)
   HIPCHK(hipEventSynchronize(ctx->pix_ev));
@@ -203,7 +211,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   HIPCHK(hipMemcpyAsync(ctx->wpix.p, ctx->pix_pinned, npix * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(ctx->pix_ev, st));
   HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), st));
-  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(unsigned long long), st));
+  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
   WaveArgs a{};
   float4* base = static_cast<float4*>(ctx->wstate.p);
   const size_t S = ctx->wslots;
@@ -223,6 +231,8 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   a.max_depth = p->max_depth;
   a.counters = static_cast<unsigned long long*>(ctx->counters.p);
   a.err = static_cast<int*>(ctx->errflag.p);
+  static const int refill = [] { const char* e = getenv("RTGPU_REFILL"); return e ? std::max(1, atoi(e)) : 16; }();
+  a.refill = refill;
   WavePlan plan{};
   plan.spp = spp;
   plan.samples_per_batch = spb;
@@ -230,6 +240,22 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   plan.max_depth = p->max_depth;
   plan.num_cus = ctx->num_cus;
   plan.probe_host = ctx->probe_pinned;
+  ctx->tev_used = 0;
+  if (ctx->timing) {
+    // worst case: 4 events per bounce per batch
+    const size_t batches = (spp + spb - 1) / spb;
+    const size_t want = std::min<size_t>(MAX_TIMING_EVENTS, batches * size_t(std::max(1, p->max_depth)) * 4 + 4);
+    while (ctx->tev.size() < want) {
+      hipEvent_t e = nullptr;
+      HIPCHK(hipEventCreate(&e));
+      ctx->tev.push_back(e);
+    }
+    ctx->tev_class.resize(ctx->tev.size());
+    plan.events = ctx->tev.data();
+    plan.ev_class = ctx->tev_class.data();
+    plan.max_events = int(ctx->tev.size());
+    plan.num_events = &ctx->tev_used;
+  }
   const int stack = ctx->host.stack_needed <= 32 ? 32 : 64;
   if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(hipEventRecord(ctx->kev0, st));
@@ -248,7 +274,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
       *ms = f;
     }
     if (count)
-      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, CNT_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   }
   return RT_OK;
 }
@@ -279,7 +305,7 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
   const size_t stride = size_t(ntiles) * 256 * 3;
   if ((rc = ensure(ctx, ctx->tiles, tiles.size() * sizeof(int4)))) return rc;
   if (!count && (rc = ensure(ctx, ctx->partial, size_t(chunks) * stride * sizeof(double)))) return rc;
-  if ((rc = ensure(ctx, ctx->counters, 16 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ensure(ctx, ctx->counters, CNT_WORDS * sizeof(unsigned long long)))) return rc;
   if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
   // Stage through pinned memory; wait for the previous upload to finish reading it.
   HIPCHK(hipEventSynchronize(ctx->tiles_ev));
@@ -294,7 +320,7 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
   HIPCHK(hipMemcpyAsync(ctx->tiles.p, ctx->tiles_pinned, tiles.size() * sizeof(int4), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(ctx->tiles_ev, st));
   HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), st));
-  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(unsigned long long), st));
+  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
   RenderLaunch w{};
   w.tiles = static_cast<const int4*>(ctx->tiles.p);
   w.ntiles = ntiles;
@@ -328,7 +354,7 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
       *ms = f;
     }
     if (count)
-      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, CNT_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   }
   return RT_OK;
 }
@@ -374,6 +400,7 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   if (ctx->pix_pinned) (void)hipHostFree(ctx->pix_pinned);
   if (ctx->probe_pinned) (void)hipHostFree(ctx->probe_pinned);
   (void)hipEventDestroy(ctx->pix_ev);
+  for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->kev0);
   (void)hipEventDestroy(ctx->kev1);
   (void)hipEventDestroy(ctx->ev0);
@@ -400,6 +427,7 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(leaves, leaves);
   UP(refs, refs);
   UP(ref_rank, ref_rank);
+  UP(ref_box, ref_box);
   UP(ref_top, tlas_ref_top);
   UP(spheres, spheres);
   UP(sphere_hidx, sphere_hidx);
@@ -505,13 +533,8 @@ int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms) {
   return RT_OK;
 }
 
-int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, rt_work_counts* out) {
-  if (!ctx || !cam || !out) return RT_ERR_INVALID;
-  HIPCHK(hipSetDevice(ctx->device));
-  unsigned long long c[12] = {0};
-  double ms = 0.0;
-  int rc = render_impl(ctx, cam, params, nullptr, ctx->stream, true, c, &ms);
-  if (rc) return rc;
+namespace {
+void fill_counts(const unsigned long long* c, rt_work_counts* out) {
   out->samples = c[0];
   out->rays = c[1];
   out->shadow_rays = c[2];
@@ -524,6 +547,57 @@ int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params
   out->volume_tests = c[9];
   out->material_fetches = c[10];
   out->env_lookups = c[11];
+  out->instance_box_tests = c[12];
+}
+}  // namespace
+
+int rt_count_work_by_kernel(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+                            rt_work_counts* out) {
+  if (!ctx || !cam || !out) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  unsigned long long c[CNT_WORDS] = {0};
+  double ms = 0.0;
+  int rc = render_impl(ctx, cam, params, nullptr, ctx->stream, true, c, &ms);
+  if (rc) return rc;
+  for (int k = 0; k < 3; ++k) fill_counts(c + k * CNT_BLOCK, out + k);
+  return RT_OK;
+}
+
+int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, rt_work_counts* out) {
+  if (!out) return RT_ERR_INVALID;
+  rt_work_counts k[3];
+  int rc = rt_count_work_by_kernel(ctx, cam, params, k);
+  if (rc) return rc;
+  const uint64_t* a = reinterpret_cast<const uint64_t*>(&k[0]);
+  const uint64_t* b = reinterpret_cast<const uint64_t*>(&k[1]);
+  const uint64_t* d = reinterpret_cast<const uint64_t*>(&k[2]);
+  uint64_t* o = reinterpret_cast<uint64_t*>(out);
+  for (size_t i = 0; i < sizeof(rt_work_counts) / sizeof(uint64_t); ++i) o[i] = a[i] + b[i] + d[i];
+  return RT_OK;
+}
+
+int rt_set_kernel_timing(rt_ctx* ctx, int enable) {
+  if (!ctx) return RT_ERR_INVALID;
+  ctx->timing = enable != 0;
+  return RT_OK;
+}
+
+int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out) {
+  if (!ctx || !out) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  std::memset(out, 0, sizeof(*out));
+  if (ctx->tev_used == 0) return set_err(ctx, RT_ERR_INVALID, "no timed render recorded (rt_set_kernel_timing)");
+  HIPCHK(hipEventSynchronize(ctx->tev[ctx->tev_used - 1]));
+  double* ms[3] = {&out->extend_ms, &out->shade_ms, &out->shadow_ms};
+  int32_t* nl[3] = {&out->extend_launches, &out->shade_launches, &out->shadow_launches};
+  for (int i = 0; i + 1 < ctx->tev_used; ++i) {
+    const int c = ctx->tev_class[i];
+    if (c > KC_SHADOW) continue;
+    float f = 0.f;
+    HIPCHK(hipEventElapsedTime(&f, ctx->tev[i], ctx->tev[i + 1]));
+    *ms[c] += f;
+    *nl[c] += 1;
+  }
   return RT_OK;
 }
 

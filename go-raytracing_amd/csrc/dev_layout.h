@@ -155,12 +155,22 @@ struct DEnv {
   const float* conditional;  // height*(width+1)
 };
 
+// World-space culling box of a TLAS ref (32 B).  Instances whose wrapper
+// chain is box-consistent (no RotateX/RotateZ, whose BoundingBox rotates the
+// opposite way to Hit, transform.go:201-268) get their padded wrapper
+// bbox; every other ref gets an infinite box (never culled).
+struct alignas(16) DRefBox {
+  float lo[3], pad0;
+  float hi[3], pad1;
+};
+
 // Everything the kernels need, passed by value as a kernel argument.
 struct DScene {
   const DNode* nodes;
   const DLeaf* leaves;
   const uint32_t* refs;
   const int32_t* ref_rank;     // DFS rank of each TLAS ref (tie rule)
+  const DRefBox* ref_box;      // per ref: world-space culling box
   const DSphere* spheres;
   const DQuad* quads;
   const DTri* tris;

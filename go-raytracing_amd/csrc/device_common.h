@@ -291,7 +291,7 @@ __device__ __forceinline__ bool accept(const DScene& sc, float t, int kind, int 
 
 // Work counters for the instrumented variant (rt_count_work).
 struct Cnt {
-  uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env;
+  uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env, ibox;
 };
 
 // Volume.Hit (volume.go:34-79) against a boundary given as an instance chain
@@ -363,7 +363,7 @@ constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the sta
 
 // Resumable traversal state (one lane, one ray).
 struct Trav {
-  V3 wo, wd;             // world-space ray (instances / volumes / restore)
+  V3 wo, wd, winv;       // world-space ray (instances / volumes / restore)
   TRay cr;               // current-space ray (object space inside an instance)
   float time, tmin, tmax;
   uint32_t key, bounce, voldom;
@@ -393,6 +393,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, V3 wo, V3 wd
     }
   }
   T.cr = make_tray(wo, wd);
+  T.winv = T.cr.inv;
   T.cur_inst = -1; T.cur_ref = -1; T.sp = 0;
   T.item = ITEM_NONE; T.lf = ITEM_NONE;
   float tn;
@@ -448,6 +449,11 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* st
     } else {
       T.item = pop();
     }
+    // leaving an instance with nothing postponed: restore the world ray inline
+    while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END && T.lf == ITEM_NONE) {
+      T.cr.o = T.wo; T.cr.d = T.wd; T.cr.inv = T.winv; T.cur_inst = -1; T.cur_ref = -1;
+      T.item = pop();
+    }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
     if (!__any(T.lf == ITEM_NONE)) break;   // every lane holds a postponed item
   }
@@ -475,6 +481,13 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* st
           if (kCount) cnt.sph++;
           ok = sphere_t(sc.spheres[pi], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
         } else if (pk == PK_INSTANCE) {
+          // world-space cull on the instance's own (padded) bbox before
+          // paying for the instance fetch + object-space root test
+          const float4* bp = reinterpret_cast<const float4*>(sc.ref_box + pos);
+          const float4 lo = bp[0], hi = bp[1];
+          float tn;
+          if (kCount) cnt.ibox++;
+          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : best.t, tn)) continue;
           if (!push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos))) return TRAV_DONE;
           continue;
         } else if (kVol && pk == PK_VOLUME) {
@@ -511,7 +524,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* st
         T.item = bb.root_item;
       }
     } else {  // ITEM_INST_END: back to the world-space ray
-      T.cr = make_tray(T.wo, T.wd); T.cur_inst = -1; T.cur_ref = -1;
+      T.cr.o = T.wo; T.cr.d = T.wd; T.cr.inv = T.winv; T.cur_inst = -1; T.cur_ref = -1;
     }
     T.lf = ITEM_NONE;
     // ITEM_NONE here only means the stack was empty when this lane last

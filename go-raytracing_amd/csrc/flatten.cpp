@@ -171,6 +171,7 @@ struct Flattener {
         int i = add_prim(g);
         S.refs.push_back((uint32_t(prim_kind(H(g).kind)) << REF_SHIFT) | uint32_t(i));
         S.ref_rank.push_back(0);
+        S.ref_box.push_back(infinite_ref_box());
         S.ref_top.push_back(-1);
       }
       lf.info = make_leaf_info(int(prims.size()), PK_MIXED, ntests);
@@ -258,6 +259,38 @@ struct Flattener {
     return id;
   }
 
+  static DRefBox infinite_ref_box() {
+    const float inf = std::numeric_limits<float>::infinity();
+    DRefBox b{};
+    for (int a = 0; a < 3; ++a) { b.lo[a] = -inf; b.hi[a] = inf; }
+    return b;
+  }
+
+  // The wrapper's own bbox (what the enclosing world leaf box is the union
+  // of), padded outward so the fp32 world-space test is conservative against
+  // the object-space BLAS root test it saves.  Only for chains whose bboxes
+  // contain the objects Hit actually sees: RotateX/RotateZ rotate their bbox
+  // by +theta but the ray by +theta too (transform.go:201-268), so the
+  // effective object lies outside its bbox and is never culled here.
+  DRefBox instance_cull_box(const rt_hittable& h, int inst) {
+    const DInstance& in = S.instances[inst];
+    for (int k = 0; k < in.nwrap; ++k)
+      if (in.kind[k] == W_ROT_X || in.kind[k] == W_ROT_Z) return infinite_ref_box();
+    double ext = 0.0;
+    for (int a = 0; a < 3; ++a) {
+      const double lo = h.bbox[2 * a], hi = h.bbox[2 * a + 1];
+      if (!(lo <= hi) || !std::isfinite(lo) || !std::isfinite(hi)) return infinite_ref_box();
+      ext = std::max(ext, std::max(hi - lo, std::max(std::fabs(lo), std::fabs(hi))));
+    }
+    const double pad = 1e-5 * ext + 1e-6;
+    DRefBox b{};
+    for (int a = 0; a < 3; ++a) {
+      b.lo[a] = round_down(h.bbox[2 * a] - pad);
+      b.hi[a] = round_up(h.bbox[2 * a + 1] + pad);
+    }
+    return b;
+  }
+
   // Collect a wrapper chain starting at g (outermost first); returns inner.
   int make_instance(int g) {
     DInstance in{};
@@ -326,6 +359,8 @@ struct Flattener {
     }
     S.refs.push_back(ref);
     S.ref_rank.push_back(rank);
+    S.ref_box.push_back((ref >> REF_SHIFT) == uint32_t(PK_INSTANCE) ? instance_cull_box(h, int(ref & REF_MASK))
+                                                                     : infinite_ref_box());
     S.ref_top.push_back(g);
     return true;
   }

@@ -12,6 +12,7 @@ struct HostScene {
   std::vector<DLeaf> leaves;
   std::vector<uint32_t> refs;
   std::vector<int32_t> ref_rank;      // per ref (TLAS refs: DFS rank; others 0)
+  std::vector<DRefBox> ref_box;      // per ref: instance culling box (infinite otherwise)
   std::vector<int32_t> ref_top;       // per ref: top-level hittable index
   std::vector<DSphere> spheres;
   std::vector<int32_t> sphere_hidx;

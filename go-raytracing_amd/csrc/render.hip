@@ -75,6 +75,7 @@ __global__ __launch_bounds__(256) void render_kernel(DScene sc, DCamera cam, Ren
     atomicAdd(c + 9, (unsigned long long)cnt.vol);
     atomicAdd(c + 10, (unsigned long long)cnt.mat);
     atomicAdd(c + 11, (unsigned long long)cnt.env);
+    atomicAdd(c + 12, (unsigned long long)cnt.ibox);
   }
 }
 

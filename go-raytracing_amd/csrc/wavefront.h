@@ -31,6 +31,7 @@ struct WaveArgs {
   int32_t max_depth;
   unsigned long long* counters;
   int* err;
+  int32_t refill;   // idle lanes per wave that trigger a queue fetch
 };
 
 struct WavePlan {
@@ -40,7 +41,18 @@ struct WavePlan {
   int32_t max_depth;
   int32_t num_cus;
   uint32_t* probe_host;     // pinned word for the long-tail early exit
+  // Per-launch timing (rt_set_kernel_timing): an event is recorded before
+  // every extend/shade/shadow launch and after every shadow launch;
+  // ev_class[i] names the kernel running between events i and i+1.
+  hipEvent_t* events;       // nullptr: timing off
+  uint8_t* ev_class;
+  int max_events;
+  int* num_events;
 };
+
+enum : uint8_t { KC_EXTEND = 0, KC_SHADE = 1, KC_SHADOW = 2, KC_OTHER = 3 };
+// Counter blocks (16 x u64 each): one per kernel class.
+constexpr int CNT_BLOCK = 16;
 
 hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs& a, const WavePlan& plan, int stack,
                             bool count, float* out, int accumulate, hipStream_t st);

@@ -62,6 +62,7 @@ __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n
   atomicAdd(c + 9, (unsigned long long)n.vol);
   atomicAdd(c + 10, (unsigned long long)n.mat);
   atomicAdd(c + 11, (unsigned long long)n.env);
+  atomicAdd(c + 12, (unsigned long long)n.ibox);
 }
 
 // ---------------------------------------------------------------- camera
@@ -99,17 +100,16 @@ __global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, uint32_
 // ---------------------------------------------------------------- refill
 // Persistent traversal lanes: when at least kRefill lanes of a wave are idle,
 // the wave grabs that many queue entries with one atomic (ballot + mbcnt).
-constexpr int kRefill = 16;
 
 struct Fetch {
   uint32_t idx;      // queue index for this lane (valid if < n)
   bool exhausted;    // wave-uniform: the queue is drained
 };
-__device__ __forceinline__ Fetch wave_fetch(bool idle, uint32_t* ctr, uint32_t n) {
+__device__ __forceinline__ Fetch wave_fetch(bool idle, uint32_t* ctr, uint32_t n, int refill) {
   Fetch f{0xFFFFFFFFu, false};
   const unsigned long long m = __ballot(idle);
   const int nidle = __popcll(m);
-  if (nidle < kRefill) return f;
+  if (nidle < refill) return f;
   const int lane = __lane_id();
   const int leader = __ffsll(m) - 1;
   uint32_t base = 0;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uin
   bool exhausted = false;
   for (;;) {
     if (!exhausted) {
-      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n);
+      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n, a.refill);
       exhausted = f.exhausted;
       if (f.idx < n) {
         p = q[f.idx];
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uin
       }
     }
   }
-  if (kCount) add_counters(a.counters, cnt, 0);
+  if (kCount) add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
 }
 
 // ---------------------------------------------------------------- shade
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs 
     wave_push(cont, p, nq, ncount);
     wave_push(want_shadow, p, a.shq, a.shcount);
   }
-  if (kCount) add_counters(a.counters, cnt, 0);
+  if (kCount) add_counters(a.counters + KC_SHADE * CNT_BLOCK, cnt, 0);
 }
 
 // ---------------------------------------------------------------- shadow
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256) void k_shadow(DScene sc, WaveArgs a, uint32_t*
   };
   for (;;) {
     if (!exhausted) {
-      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n);
+      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n, a.refill);
       exhausted = f.exhausted;
       if (f.idx < n) {
         p = a.shq[f.idx];
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void k_shadow(DScene sc, WaveArgs a, uint32_t*
       if (s != TRAV_RUNNING && finish_ray(s)) p = ITEM_NONE;
     }
   }
-  if (kCount) add_counters(a.counters, cnt, 0);
+  if (kCount) add_counters(a.counters + KC_SHADOW * CNT_BLOCK, cnt, 0);
 }
 
 // ---------------------------------------------------------------- accumulate
@@ -463,6 +463,15 @@ static int grid_for(const void* fn, int block, size_t lds, uint32_t items, int c
   return int(need < resident ? need : resident);
 }
 
+// Record the next timing event; the interval it opens belongs to `cls`.
+static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
+  if (!plan.events) return hipSuccess;
+  int& n = *plan.num_events;
+  if (n >= plan.max_events) return hipSuccess;   // pool exhausted: later launches untimed
+  plan.ev_class[n] = cls;
+  return hipEventRecord(plan.events[n++], st);
+}
+
 template <int STACK, bool kCount, bool kVol>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
   const int cus = plan.num_cus;
@@ -482,11 +491,15 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
       uint32_t* nq = (b & 1) ? a.q0 : a.q1;
       uint32_t* cc = a.counts + (b & 1);
       uint32_t* nc = a.counts + ((b & 1) ^ 1);
+      if ((e = mark(plan, KC_EXTEND, st)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, cq, cc, nc, a.shcount,
                          a.counts + 3, a.counts + 4);
+      if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_shade<kCount>), dim3(gsh), dim3(256), 0, st, sc, cam, a, cq, cc, nq, nc);
+      if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol>), dim3(gsd), dim3(256), 0, st, sc, a, a.counts + 4,
                          a.counts + 3);
+      if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
         // long-tail scenes (RandomScene depth 50): stop once every path ended
         uint32_t left = 0;

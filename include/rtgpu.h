@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -180,7 +180,15 @@ typedef struct rt_work_counts {
   uint64_t sphere_tests, quad_tests, tri_tests, plane_tests;
   uint64_t instance_visits, volume_tests;
   uint64_t material_fetches, env_lookups;
+  uint64_t instance_box_tests; /* world-space instance culling boxes (32 B)  */
 } rt_work_counts;
+
+/* Summed per-launch durations of the wavefront kernels of the last render
+ * (HIP events on the render stream; rt_set_kernel_timing(ctx, 1) first).  */
+typedef struct rt_kernel_times {
+  double extend_ms, shade_ms, shadow_ms;
+  int32_t extend_launches, shade_launches, shadow_launches, pad;
+} rt_kernel_times;
 
 /* Sizes of the flattened device scene (rt_scene_get_info). */
 typedef struct rt_scene_info {
@@ -222,6 +230,17 @@ int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms);
 /* Instrumented run of the same kernel: traversal/prim counters. */
 int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                   rt_work_counts* out);
+
+/* Same instrumented run, counters split by kernel: out[0] = extend
+ * (closest-hit traversal, camera rays), out[1] = shade (materials, NEE
+ * set-up, HDRI lookups), out[2] = shadow (any-hit traversal).             */
+int rt_count_work_by_kernel(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+                            rt_work_counts out[3]);
+
+/* Per-launch kernel timing of subsequent renders (off by default; one HIP
+ * event before every extend/shade/shadow launch and after every shadow).   */
+int rt_set_kernel_timing(rt_ctx* ctx, int enable);
+int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out);
 
 /* RGBA8 quantisation of an accumulated sum (bucket_renderer.go:276-285):
  * c*(1/spp) -> LinearToGamma (utils.go:85-90) -> clamp [0,0.999] ->

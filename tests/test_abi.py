@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol(g, header, lib):
 
 
 def test_abi_version(g):
-    assert g.rtgpu().rt_abi_version() == 1
+    assert g.rtgpu().rt_abi_version() == 2
 
 
 def test_no_silent_cpu_fallback_without_gpu(g):
@@ -48,3 +48,25 @@ def test_scene_desc_struct_sizes(g):
     assert C.sizeof(g.RtHittable) == 4 * 4 + 6 * 8 + 16 * 8
     assert C.sizeof(g.RtMaterial) == 8 + 5 * 8
     assert C.sizeof(g.RtTexture) == 16 + 4 * 8
+
+
+def test_ctypes_mirror_matches_c_header(g, tmp_path):
+    """sizeof of every ABI struct as gcc sees include/rtgpu.h == the ctypes mirror."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    names = {"rt_hittable": g.RtHittable, "rt_material": g.RtMaterial, "rt_texture": g.RtTexture,
+             "rt_work_counts": g.RtWorkCounts, "rt_kernel_times": g.RtKernelTimes,
+             "rt_scene_info": g.RtSceneInfo, "rt_camera_desc": g.RtCameraDesc,
+             "rt_render_params": g.RtRenderParams, "rt_scene_desc": g.RtSceneDesc, "rt_stats": g.RtStats}
+    src = tmp_path / "probe.c"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    body = "".join(f'  printf("{n} %zu\\n", sizeof({n}));\n' for n in names)
+    src.write_text(f'#include <stdio.h>\n#include "rtgpu.h"\nint main(void) {{\n{body}  return 0;\n}}\n')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    sizes = dict(line.split() for line in out if line)
+    for n, cls in names.items():
+        assert int(sizes[n]) == C.sizeof(cls), n

@@ -1,0 +1,86 @@
+"""CPU checks of the host flattener and of the device path-tracing source.
+
+* tests/flatten_probe.cpp: every index the kernels dereference (node items,
+  leaf ranges, refs, instance -> BLAS, volume boundaries, textures) is in
+  range for each scene, and the per-ref arrays (rank, culling box, top
+  object) are parallel to `refs`.
+* tests/trav_emu.cpp: device_common.h (the kernels' traversal, shading and
+  NEE code) compiled for the host with one lane per wave and random
+  wave-mates in the while-while vote, run under AddressSanitizer +
+  UBSan, and compared with the oracle's fp32 mode (same op order): the
+  per-pixel sums agree to fp32 accumulation rounding.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "go-raytracing_amd", "lib")
+CSRC = os.path.join(ROOT, "go-raytracing_amd", "csrc")
+ASSETS = os.path.join(ROOT, "assets")
+SCENES = ["simple", "random", "cornell", "cornell-smoke", "cornell-lucy", "hdri-test", "hdri-nee"]
+
+pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+
+
+def _build(tmp, src, out, sanitize=False):
+    cmd = ["g++", "-O1", "-g", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "include")]
+    if sanitize:
+        cmd += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined",
+                "-I", os.path.join(ROOT, "tests", "host_emu")]
+    cmd += [os.path.join(ROOT, "tests", src), os.path.join(CSRC, "flatten.cpp"), "-L", LIB, "-lrtscene",
+            f"-Wl,-rpath,{LIB}", "-o", str(out)]
+    subprocess.run(cmd, check=True, cwd=tmp)
+    return str(out)
+
+
+@pytest.fixture(scope="module")
+def probe(tmp_path_factory, g):
+    t = tmp_path_factory.mktemp("probe")
+    return _build(t, "flatten_probe.cpp", t / "probe")
+
+
+@pytest.fixture(scope="module")
+def emu(tmp_path_factory, g):
+    t = tmp_path_factory.mktemp("emu")
+    return _build(t, "trav_emu.cpp", t / "emu", sanitize=True)
+
+
+def _env():
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=0:verify_asan_link_order=0:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
+    return env
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_flattened_indices_in_range(probe, name):
+    r = subprocess.run([probe, name, "64", ASSETS], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    info = json.loads(r.stdout)
+    assert info["fails"] == 0, info
+    assert 0 < info["stack_needed"] <= 64
+    if name in ("cornell-lucy",):
+        assert info["culling_boxes"] == info["instances"] == 10   # RotateY/Translate/Scale only
+
+
+@pytest.mark.parametrize("name", ["simple", "cornell", "cornell-smoke", "cornell-lucy", "hdri-nee"])
+def test_device_source_under_asan_matches_oracle(emu, O, g, tmp_path, name):
+    spp, seed = 2, 77
+    out = tmp_path / f"{name}.f32"
+    r = subprocess.run([emu, name, "48", str(spp), str(seed), ASSETS, str(out)], capture_output=True, text=True,
+                       env=_env(), timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    kw = dict(width=48)
+    if name == "cornell-lucy":
+        kw.update(lucy_rings=60, lucy_cols=80)
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
+    got = np.fromfile(out, np.float32).reshape(ref.shape)
+    # same op order: only the fp32 rounding of the per-pixel sum differs
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())
