@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=0, help="0: scene default")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--blas", choices=["sah", "reference"], default="sah",
+                    help="BVH layout (mesh BLAS and world BVH): SAH (default) or the caller's topology")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented count run")
     ap.add_argument("--cpu-spp", type=int, default=48, help="spp of the CPU baseline sample")
@@ -105,6 +107,8 @@ def main():
     cam = scene.camera
     W, H, spp, depth = cam.image_width, cam.image_height, cam.samples_per_pixel, cam.max_depth
     ctx = g.Context(local if world > 1 else 0)
+    ctx.set_blas_builder(args.blas)
+    ctx.set_tlas_builder(args.blas)
     ctx.upload(scene.desc)
     info = ctx.info()
     t_build = time.time() - t_build
@@ -219,7 +223,7 @@ def main():
             "data": "synthetic (deterministic 280K-tri Lucy stand-in; scene geometry per scenes.go)",
             "config": {"workload": f"{args.scene} {W}x{H} {spp}spp depth {depth}", "scene": args.scene,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "parallelism": f"tiles-rr{world}", "buckets": len(buckets),
+                       "parallelism": f"tiles-rr{world}", "buckets": len(buckets), "blas": args.blas,
                        "triangles": info.triangles, "bvh_nodes": info.nodes,
                        "scene_build_s": round(t_build, 2), "image_finite": img_ok},
             "roofline": roofline,

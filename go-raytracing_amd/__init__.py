@@ -27,6 +27,8 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 ASSET_DIR = os.path.join(REPO_DIR, "assets")
 
 RT_OK = 0
+RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER = 1, 2
+RT_BLAS_REFERENCE, RT_BLAS_SAH = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_SCENE", -6: "RT_ERR_DEVICE"}
 
@@ -149,6 +151,7 @@ def rtgpu() -> C.CDLL:
         lib.rt_count_work_by_kernel.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
                                                 C.POINTER(RtWorkCounts)]
         lib.rt_set_kernel_timing.argtypes = [P, C.c_int]
+        lib.rt_ctx_set_option.argtypes = [P, I32, I32]
         lib.rt_last_kernel_times.argtypes = [P, C.POINTER(RtKernelTimes)]
         lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
         lib.rt_primary_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32), C.POINTER(I32),
@@ -373,6 +376,17 @@ class Context:
         self._check(self._lib.rt_count_work_by_kernel(self._h, C.byref(camera), C.byref(params), w))
         return {k: {n: int(getattr(w[i], n)) for n, _ in RtWorkCounts._fields_}
                 for i, k in enumerate(("extend", "shade", "shadow"))}
+
+    def set_option(self, key: int, value: int):
+        self._check(self._lib.rt_ctx_set_option(self._h, key, value))
+
+    def set_blas_builder(self, builder: str):
+        """Mesh BLAS layout: "sah" (default) or "reference" (the caller's BVH topology); next upload."""
+        self.set_option(RT_OPT_BLAS_BUILDER, {"reference": RT_BLAS_REFERENCE, "sah": RT_BLAS_SAH}[builder])
+
+    def set_tlas_builder(self, builder: str):
+        """World BVH layout: "sah" (default) or "reference"; next upload."""
+        self.set_option(RT_OPT_TLAS_BUILDER, {"reference": RT_BLAS_REFERENCE, "sah": RT_BLAS_SAH}[builder])
 
     def set_kernel_timing(self, enable: bool = True):
         self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))

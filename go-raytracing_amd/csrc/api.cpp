@@ -56,6 +56,7 @@ struct rt_ctx {
   std::vector<hipEvent_t> tev;
   std::vector<uint8_t> tev_class;
   int tev_used = 0;
+  FlattenOptions fopt;
 };
 
 namespace {
@@ -411,13 +412,28 @@ void rt_ctx_destroy(rt_ctx* ctx) {
 
 const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->error.c_str() : "null context"; }
 
+int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
+  if (!ctx) return RT_ERR_INVALID;
+  if (key == RT_OPT_BLAS_BUILDER) {
+    if (value != RT_BLAS_REFERENCE && value != RT_BLAS_SAH) return set_err(ctx, RT_ERR_INVALID, "bad BLAS builder");
+    ctx->fopt.blas_builder = value == RT_BLAS_SAH ? BLAS_SAH : BLAS_REFERENCE;
+    return RT_OK;
+  }
+  if (key == RT_OPT_TLAS_BUILDER) {
+    if (value != RT_BLAS_REFERENCE && value != RT_BLAS_SAH) return set_err(ctx, RT_ERR_INVALID, "bad TLAS builder");
+    ctx->fopt.tlas_builder = value == RT_BLAS_SAH ? BLAS_SAH : BLAS_REFERENCE;
+    return RT_OK;
+  }
+  return set_err(ctx, RT_ERR_INVALID, "unknown option " + std::to_string(key));
+}
+
 int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   if (!ctx) return RT_ERR_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   free_scene(ctx);
   std::string err;
-  int rc = flatten_scene(scene, ctx->host, err);
+  int rc = flatten_scene(scene, ctx->host, err, ctx->fopt);
   if (rc) return set_err(ctx, rc, err);
   HostScene& h = ctx->host;
   DScene& d = ctx->dscene;
@@ -445,6 +461,9 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(materials, materials);
   UP(textures, textures);
   UP(lights, lights);
+  UP(sphere_rank, sphere_rank);
+  UP(quad_rank, quad_rank);
+  UP(tri_rank, tri_rank);
   UP(env_texels, env.texels);
   UP(env_pdf, env.pdf);
   UP(env_marginal, env.marginal);

@@ -182,6 +182,10 @@ struct DScene {
   const DMaterial* materials;
   const DTexture* textures;
   const DLight* lights;
+  // per-primitive DFS rank inside its BLAS (tie rule; read on exact t ties only)
+  const int32_t* sphere_rank;
+  const int32_t* quad_rank;
+  const int32_t* tri_rank;
   // hit -> hittable index maps (parity probe)
   const int32_t* tlas_ref_top;   // per TLAS ref: top-level hittable index
   const int32_t* sphere_hidx;

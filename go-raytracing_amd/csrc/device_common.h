@@ -272,6 +272,13 @@ __device__ __forceinline__ bool closed_kind(int k) { return k == PK_QUAD || k ==
 __device__ __forceinline__ int obj_rank(const DScene& sc, int refpos) {
   return refpos >= 0 ? sc.ref_rank[refpos] : sc.planes[-1 - refpos].rank;
 }
+// Rank of a primitive inside its BLAS in the reference's DFS order.  primpos
+// is the primitive array index, or (bit 31 set) the refs index for mixed
+// leaves.  Only read on exact t ties.
+__device__ __forceinline__ int prim_rank(const DScene& sc, int kind, int primpos) {
+  if (primpos < 0) return sc.ref_rank[primpos & 0x7FFFFFFF];
+  return kind == PK_TRI ? sc.tri_rank[primpos] : kind == PK_QUAD ? sc.quad_rank[primpos] : sc.sphere_rank[primpos];
+}
 // Is candidate (kind, refpos, primpos) preferred over the best at equal t?
 // Rare (exact float ties), scalar arguments only.
 __device__ __forceinline__ bool tie_wins(const DScene& sc, int kind, int refpos, int primpos, int bkind, int brefpos,
@@ -279,8 +286,13 @@ __device__ __forceinline__ bool tie_wins(const DScene& sc, int kind, int refpos,
   const bool cc = closed_kind(kind), bc = closed_kind(bkind);
   if (cc != bc) return cc;
   const int rc = obj_rank(sc, refpos), rb = obj_rank(sc, brefpos);
-  if (rc == rb && primpos == bprimpos) return false;
-  const bool later = (rc > rb) || (rc == rb && primpos > bprimpos);
+  bool later;
+  if (rc == rb) {   // same top-level object: inside one instance BLAS
+    if (primpos == bprimpos) return false;
+    later = prim_rank(sc, kind, primpos) > prim_rank(sc, bkind, bprimpos);
+  } else {
+    later = rc > rb;
+  }
   return cc ? later : !later;
 }
 __device__ __forceinline__ bool accept(const DScene& sc, float t, int kind, int refpos, int primpos, const Best& b) {
@@ -497,7 +509,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* st
         if (!ok) continue;
         if (kAny) return TRAV_ANYHIT;
         const int refpos = world ? pos : T.cur_ref;
-        const int primpos = world ? 0 : pos;
+        const int primpos = world ? 0 : (kind == PK_MIXED ? int(uint32_t(pos) | 0x80000000u) : pos);
         if (accept(sc, t, pk, refpos, primpos, best)) {
           best.t = t; best.kind = pk; best.idx = int(pi); best.inst = T.cur_inst;
           best.refpos = refpos; best.primpos = primpos;

@@ -17,6 +17,7 @@
 // device tie rule (render.hip, Best/accept) uses them.
 #include "flatten.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -77,7 +78,11 @@ struct Flattener {
   std::map<int, int> vol_ids;       // graph index of volume -> vol_id
   uint32_t empty_leaf = 0;
 
-  Flattener(const rt_scene_desc* desc, HostScene& s, std::string& e) : d(desc), S(s), err(e) {}
+  FlattenOptions opt;
+  int blas_rank = 0;                // DFS rank counter of the BLAS being built
+
+  Flattener(const rt_scene_desc* desc, HostScene& s, std::string& e, const FlattenOptions& o)
+      : d(desc), S(s), err(e), opt(o) {}
 
   bool fail(int code, const std::string& m) {
     if (status == RT_OK) { status = code; err = m; }
@@ -103,6 +108,7 @@ struct Flattener {
     s.mat = h.material;
     S.spheres.push_back(s);
     S.sphere_hidx.push_back(g);
+    S.sphere_rank.push_back(0);
     return int(S.spheres.size()) - 1;
   }
   int add_quad(int g) {
@@ -116,6 +122,7 @@ struct Flattener {
     q.D = float(h.p[15]);
     q.mat = h.material;
     S.quads.push_back(q);
+    S.quad_rank.push_back(0);
     S.quad_hidx.push_back(g);
     return int(S.quads.size()) - 1;
   }
@@ -135,6 +142,7 @@ struct Flattener {
     S.tris.push_back(t);
     S.tri_aux.push_back(ax);
     S.tri_hidx.push_back(g);
+    S.tri_rank.push_back(0);
     return int(S.tris.size()) - 1;
   }
   int prim_kind(int k) const {
@@ -147,6 +155,12 @@ struct Flattener {
       case RT_TRIANGLE: return add_tri(g);
     }
     return -1;
+  }
+
+  void set_prim_rank(int kind, int i, int r) {
+    if (kind == RT_SPHERE) S.sphere_rank[i] = r;
+    else if (kind == RT_QUAD) S.quad_rank[i] = r;
+    else if (kind == RT_TRIANGLE) S.tri_rank[i] = r;
   }
 
   // Leaf over a list of primitive graph indices (BLAS level).  Homogeneous
@@ -162,7 +176,11 @@ struct Flattener {
     DLeaf lf{};
     if (homo) {
       int first = -1;
-      for (int g : prims) { int i = add_prim(g); if (first < 0) first = i; }
+      for (int g : prims) {
+        int i = add_prim(g);
+        set_prim_rank(H(g).kind, i, blas_rank++);
+        if (first < 0) first = i;
+      }
       lf.first = uint32_t(first);
       lf.info = make_leaf_info(int(prims.size()), prim_kind(k0), ntests);
     } else {
@@ -170,7 +188,7 @@ struct Flattener {
       for (int g : prims) {
         int i = add_prim(g);
         S.refs.push_back((uint32_t(prim_kind(H(g).kind)) << REF_SHIFT) | uint32_t(i));
-        S.ref_rank.push_back(0);
+        S.ref_rank.push_back(blas_rank++);
         S.ref_box.push_back(infinite_ref_box());
         S.ref_top.push_back(-1);
       }
@@ -227,13 +245,165 @@ struct Flattener {
   }
   uint32_t blas_child(int g, int depth, int& maxdepth) { return blas_item(g, depth, maxdepth); }
 
+  // Primitives of a graph BVH in the reference's left-first DFS order (each
+  // once; the BVHNode{leaf,leaf} wrapper visits its leaf twice with the same
+  // result).  False unless every primitive is a triangle.
+  bool collect_triangles(int g, std::vector<int>& out, int depth = 0) {
+    if (depth > 200 || !valid_index(g)) return false;
+    const rt_hittable& h = H(g);
+    if (h.kind == RT_TRIANGLE) { out.push_back(g); return true; }
+    if (h.kind == RT_BVH_NODE) {
+      if (h.a == h.b) return collect_triangles(h.a, out, depth + 1);
+      return collect_triangles(h.a, out, depth + 1) && collect_triangles(h.b, out, depth + 1);
+    }
+    if (h.kind == RT_BVH_LEAF || h.kind == RT_LIST) {
+      if (!child_range(h)) return false;
+      for (int i = 0; i < h.b; ++i)
+        if (!collect_triangles(d->children[h.a + i], out, depth + 1)) return false;
+      return true;
+    }
+    return false;
+  }
+
+  // ---------------------------------------------------------- SAH BLAS
+  struct SahPrim {
+    double lo[3], hi[3], c[3];
+    int g, rank;
+  };
+  static double half_area(const Box& b) {
+    if (b.empty()) return 0.0;
+    const double x = b.b[1] - b.b[0], y = b.b[3] - b.b[2], z = b.b[5] - b.b[4];
+    return x * y + y * z + z * x;
+  }
+  static void grow(Box& b, const SahPrim& p) {
+    for (int a = 0; a < 3; ++a) {
+      if (p.lo[a] < b.b[2 * a]) b.b[2 * a] = p.lo[a];
+      if (p.hi[a] > b.b[2 * a + 1]) b.b[2 * a + 1] = p.hi[a];
+    }
+  }
+
+  uint32_t sah_blas(const std::vector<int>& mesh, int& maxdepth) {
+    std::vector<SahPrim> P(mesh.size());
+    for (size_t i = 0; i < mesh.size(); ++i) {
+      const rt_hittable& h = H(mesh[i]);
+      for (int a = 0; a < 3; ++a) {
+        P[i].lo[a] = h.bbox[2 * a];
+        P[i].hi[a] = h.bbox[2 * a + 1];
+        P[i].c[a] = 0.5 * (P[i].lo[a] + P[i].hi[a]);
+      }
+      P[i].g = mesh[i];
+      P[i].rank = int(i);
+    }
+    Box box;
+    return sah_node(P, 0, int(P.size()), 1, maxdepth, box);
+  }
+
+  // Binned SAH (16 bins per axis, traversal cost 2, intersection cost 1 per
+  // triangle, leaves of at most 4).  Node boxes = union of the triangles'
+  // fp64 bboxes (with the reference's padToMinimums), rounded outward.
+  uint32_t sah_node(std::vector<SahPrim>& P, int b, int e, int depth, int& maxdepth, Box& box) {
+    if (depth > maxdepth) maxdepth = depth;
+    const int n = e - b;
+    Box cb;
+    for (int i = b; i < e; ++i) {
+      grow(box, P[i]);
+      for (int a = 0; a < 3; ++a) {
+        if (P[i].c[a] < cb.b[2 * a]) cb.b[2 * a] = P[i].c[a];
+        if (P[i].c[a] > cb.b[2 * a + 1]) cb.b[2 * a + 1] = P[i].c[a];
+      }
+    }
+    constexpr int kBins = 16, kMaxLeaf = 4;
+    constexpr double kTrav = 2.0;   // one node visit (two boxes, 64 B) ~ two triangle tests
+    int best_axis = -1, best_split = 0;
+    double best_cost = std::numeric_limits<double>::infinity();
+    const double pa = half_area(box);
+    for (int a = 0; a < 3; ++a) {
+      const double lo = cb.b[2 * a], ext = cb.b[2 * a + 1] - lo;
+      if (!(ext > 0.0)) continue;
+      Box bb[kBins];
+      int cnt[kBins] = {0};
+      for (int i = b; i < e; ++i) {
+        int k = int((P[i].c[a] - lo) / ext * kBins);
+        k = std::min(std::max(k, 0), kBins - 1);
+        cnt[k]++;
+        grow(bb[k], P[i]);
+      }
+      double right_area[kBins];
+      int right_cnt[kBins];
+      Box acc;
+      int c = 0;
+      for (int k = kBins - 1; k > 0; --k) {
+        acc.merge(bb[k]);
+        c += cnt[k];
+        right_area[k] = half_area(acc);
+        right_cnt[k] = c;
+      }
+      acc = Box();
+      c = 0;
+      for (int k = 0; k < kBins - 1; ++k) {
+        acc.merge(bb[k]);
+        c += cnt[k];
+        if (c == 0 || right_cnt[k + 1] == 0) continue;
+        const double cost = kTrav + (half_area(acc) * c + right_area[k + 1] * right_cnt[k + 1]) / std::max(pa, 1e-300);
+        if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = k + 1; }
+      }
+    }
+    if (n <= kMaxLeaf && (best_axis < 0 || double(n) <= best_cost)) {
+      std::vector<int> prims;
+      for (int i = b; i < e; ++i) prims.push_back(P[i].g);
+      const uint32_t item = make_prim_leaf(prims, 1);
+      // make_prim_leaf ranked them in leaf order; the tie rule needs the
+      // reference DFS order instead
+      const DLeaf& lf = S.leaves[item & ITEM_MASK];
+      for (int i = b; i < e; ++i) S.tri_rank[lf.first + (i - b)] = P[i].rank;
+      return item;
+    }
+    int mid;
+    if (best_axis >= 0 && depth < 48) {
+      const double lo = cb.b[2 * best_axis], ext = cb.b[2 * best_axis + 1] - lo;
+      SahPrim* m = std::partition(P.data() + b, P.data() + e, [&](const SahPrim& p) {
+        int k = int((p.c[best_axis] - lo) / ext * kBins);
+        k = std::min(std::max(k, 0), kBins - 1);
+        return k < best_split;
+      });
+      mid = int(m - P.data());
+    } else {   // degenerate centroids / too deep: median split on the widest axis
+      int a = 0;
+      for (int k = 1; k < 3; ++k)
+        if (cb.b[2 * k + 1] - cb.b[2 * k] > cb.b[2 * a + 1] - cb.b[2 * a]) a = k;
+      mid = b + n / 2;
+      std::nth_element(P.begin() + b, P.begin() + mid, P.begin() + e,
+                       [a](const SahPrim& x, const SahPrim& y) { return x.c[a] < y.c[a]; });
+    }
+    if (mid <= b || mid >= e) mid = b + n / 2;
+    const int idx = int(S.nodes.size());
+    S.nodes.push_back(DNode{});
+    Box lb, rb;
+    const uint32_t li = sah_node(P, b, mid, depth + 1, maxdepth, lb);
+    const uint32_t ri = sah_node(P, mid, e, depth + 1, maxdepth, rb);
+    DNode& nd = S.nodes[idx];
+    store_box(nd.l, lb);
+    store_box(nd.r, rb);
+    nd.litem = li;
+    nd.ritem = ri;
+    return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
+  }
+
   int build_blas(int g) {
     auto it = blas_memo.find(g);
     if (it != blas_memo.end()) return it->second;
     const rt_hittable& h = H(g);
     DBvh b{};
     int depth = 0;
-    if (h.kind == RT_LIST) {          // HittableList.Hit: linear, no bbox test
+    blas_rank = 0;
+    std::vector<int> mesh;
+    if (h.kind == RT_BVH_NODE && opt.blas_builder == BLAS_SAH && collect_triangles(g, mesh) &&
+        int(mesh.size()) >= opt.sah_min_prims) {
+      // Same triangles, same closest hit (order-independent tie rule with
+      // the reference DFS ranks), better tree: binned SAH.
+      b.root_item = sah_blas(mesh, depth);
+      b.check_box = 1;
+    } else if (h.kind == RT_LIST) {          // HittableList.Hit: linear, no bbox test
       b.root_item = make_prim_leaf(children_of(h), 1);
       b.check_box = 0;
     } else if (h.kind == RT_BVH_LEAF) {
@@ -448,6 +618,160 @@ struct Flattener {
     return tlas_leaf({g}, 1, box);
   }
 
+  // ---------------------------------------------------------- SAH TLAS
+  // The world BVH rebuilt over the same top-level objects, one object per
+  // leaf.  Every object keeps what the reference's traversal attaches to it:
+  // its DFS rank (tie rule), its leaf's test count (volume double test) and
+  // its own bbox as the culling box.  Not used when a RotateX/RotateZ
+  // wrapper exists (their bbox does not contain what Hit sees,
+  // transform.go:201-351, so only the reference's grouping reproduces which
+  // rays reach them).
+  struct TopObj {
+    int g, rank, ntests;
+    double lo[3], hi[3], c[3];
+  };
+  std::vector<TopObj> top_objs;
+
+  bool tlas_sah_ok() const {
+    for (int i = 0; i < d->num_hittables; ++i) {
+      const int k = d->hittables[i].kind;
+      if (k == RT_ROTATE_X || k == RT_ROTATE_Z) return false;
+    }
+    return true;
+  }
+
+  void top_leaf_objs(const std::vector<int>& objs, int ntests) {
+    for (int g : objs) {
+      const int rank = rank_counter++;
+      const rt_hittable& h = H(g);
+      if (h.kind == RT_PLANE) {
+        DPlane p{};
+        p.px = float(h.p[0]); p.py = float(h.p[1]); p.pz = float(h.p[2]);
+        p.nx = float(h.p[3]); p.ny = float(h.p[4]); p.nz = float(h.p[5]);
+        p.mat = h.material;
+        p.rank = rank;
+        S.planes.push_back(p);
+        S.plane_hidx.push_back(g);
+        continue;
+      }
+      TopObj o{};
+      o.g = g; o.rank = rank; o.ntests = ntests;
+      for (int a = 0; a < 3; ++a) {
+        o.lo[a] = h.bbox[2 * a];
+        o.hi[a] = h.bbox[2 * a + 1];
+        o.c[a] = 0.5 * (o.lo[a] + o.hi[a]);
+        if (!std::isfinite(o.c[a])) { o.lo[a] = -kInf; o.hi[a] = kInf; o.c[a] = 0.0; }
+      }
+      top_objs.push_back(o);
+    }
+  }
+
+  // Same walk (and rank order) as tlas_item / tlas_leaf.
+  void collect_top(int g, int depth) {
+    if (status) return;
+    if (depth > 200) { fail(RT_ERR_UNSUPPORTED, "world BVH too deep"); return; }
+    const rt_hittable& h = H(g);
+    if (h.kind == RT_BVH_NODE) {
+      if (!valid_index(h.a) || !valid_index(h.b)) { fail(RT_ERR_INVALID, "bad BVH child"); return; }
+      if (h.a == h.b) {
+        const rt_hittable& c = H(h.a);
+        if (c.kind == RT_BVH_LEAF) { top_leaf_objs(children_of(c), 2); return; }
+        if (c.kind == RT_BVH_NODE) { fail(RT_ERR_UNSUPPORTED, "BVH node with identical subtree children"); return; }
+        top_leaf_objs({h.a}, 2);
+        return;
+      }
+      collect_top(h.a, depth + 1);
+      collect_top(h.b, depth + 1);
+      return;
+    }
+    if (h.kind == RT_BVH_LEAF || h.kind == RT_LIST) { top_leaf_objs(children_of(h), 1); return; }
+    top_leaf_objs({g}, 1);
+  }
+
+  uint32_t sah_tlas(Box& root) {
+    collect_top(d->root, 1);
+    if (status) return empty_leaf;
+    for (const TopObj& o : top_objs) {   // BLASes first (their refs stay out of the world leaves)
+      const rt_hittable& h = H(o.g);
+      int cur = h.kind == RT_VOLUME ? h.a : o.g;
+      while (valid_index(cur) && is_wrapper(H(cur).kind)) cur = H(cur).a;
+      if (!is_prim(h.kind) && valid_index(cur) &&
+          (H(cur).kind == RT_LIST || H(cur).kind == RT_BVH_NODE || H(cur).kind == RT_BVH_LEAF))
+        build_blas(cur);
+      if (status) return empty_leaf;
+    }
+    if (top_objs.empty()) return empty_leaf;
+    max_leaf_inst = 1;
+    return sah_top_node(0, int(top_objs.size()), 1, root);
+  }
+
+  uint32_t sah_top_node(int b, int e, int depth, Box& box) {
+    if (depth > S.tlas_depth) S.tlas_depth = depth;
+    for (int i = b; i < e; ++i) {
+      const TopObj& o = top_objs[i];
+      for (int a = 0; a < 3; ++a) {
+        if (o.lo[a] < box.b[2 * a]) box.b[2 * a] = o.lo[a];
+        if (o.hi[a] > box.b[2 * a + 1]) box.b[2 * a + 1] = o.hi[a];
+      }
+    }
+    auto make_leaf = [&]() -> uint32_t {
+      DLeaf lf{};
+      lf.first = uint32_t(S.refs.size());
+      for (int i = b; i < e; ++i)
+        if (!add_object_ref(top_objs[i].g, top_objs[i].rank)) return empty_leaf;
+      // primitives are idempotent under a repeated test; a lone volume keeps
+      // its reference leaf's count
+      lf.info = make_leaf_info(e - b, PK_MIXED, e - b == 1 ? top_objs[b].ntests : 1);
+      S.leaves.push_back(lf);
+      return (ITEM_LEAF << ITEM_SHIFT) | uint32_t(S.leaves.size() - 1);
+    };
+    if (e - b == 1) return make_leaf();
+    bool all_prims = e - b <= 4;
+    for (int i = b; i < e && all_prims; ++i) all_prims = is_prim(H(top_objs[i].g).kind);
+    // exact SAH sweep over the few top-level objects (three axes)
+    int best_axis = 0, best_mid = b + (e - b) / 2;
+    double best_cost = std::numeric_limits<double>::infinity();
+    std::vector<TopObj> tmp;
+    for (int a = 0; a < 3; ++a) {
+      std::stable_sort(top_objs.begin() + b, top_objs.begin() + e,
+                       [a](const TopObj& x, const TopObj& y) { return x.c[a] < y.c[a]; });
+      std::vector<double> right(e - b + 1, 0.0);
+      Box acc;
+      for (int i = e - 1; i > b; --i) {
+        for (int k = 0; k < 3; ++k) {
+          acc.b[2 * k] = std::min(acc.b[2 * k], top_objs[i].lo[k]);
+          acc.b[2 * k + 1] = std::max(acc.b[2 * k + 1], top_objs[i].hi[k]);
+        }
+        right[i - b] = half_area(acc) * (e - i);
+      }
+      acc = Box();
+      for (int i = b; i < e - 1; ++i) {
+        for (int k = 0; k < 3; ++k) {
+          acc.b[2 * k] = std::min(acc.b[2 * k], top_objs[i].lo[k]);
+          acc.b[2 * k + 1] = std::max(acc.b[2 * k + 1], top_objs[i].hi[k]);
+        }
+        const double cost = half_area(acc) * (i + 1 - b) + right[i + 1 - b];
+        if (cost < best_cost) { best_cost = cost; best_axis = a; best_mid = i + 1; }
+      }
+    }
+    // small groups of plain primitives may stay together (SAH: a node visit
+    // costs about two primitive tests)
+    if (all_prims && double(e - b) <= 2.0 + best_cost / std::max(half_area(box), 1e-300)) return make_leaf();
+    std::stable_sort(top_objs.begin() + b, top_objs.begin() + e,
+                     [best_axis](const TopObj& x, const TopObj& y) { return x.c[best_axis] < y.c[best_axis]; });
+    const int idx = int(S.nodes.size());
+    S.nodes.push_back(DNode{});
+    Box lb, rb;
+    const uint32_t li = sah_top_node(b, best_mid, depth + 1, lb);
+    const uint32_t ri = sah_top_node(best_mid, e, depth + 1, rb);
+    DNode& nd = S.nodes[idx];
+    store_box(nd.l, lb);
+    store_box(nd.r, rb);
+    nd.litem = li;
+    nd.ritem = ri;
+    return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
+  }
+
   void materials() {
     for (int i = 0; i < d->num_materials; ++i) {
       const rt_material& m = d->materials[i];
@@ -579,10 +903,16 @@ struct Flattener {
     S.leaves.push_back(DLeaf{0, make_leaf_info(0, PK_MIXED, 1)});
     empty_leaf = (ITEM_LEAF << ITEM_SHIFT) | 0u;
     Box root;
-    uint32_t ri = tlas_item(d->root, 1, root);
+    uint32_t ri;
+    if (opt.tlas_builder == BLAS_SAH && tlas_sah_ok()) {
+      ri = sah_tlas(root);
+      S.tlas.check_box = 1;
+    } else {
+      ri = tlas_item(d->root, 1, root);
+      S.tlas.check_box = H(d->root).kind == RT_BVH_NODE ? 1 : 0;
+    }
     if (status) return status;
     S.tlas.root_item = ri;
-    S.tlas.check_box = H(d->root).kind == RT_BVH_NODE ? 1 : 0;
     store_box(S.tlas.box, root);
     lights();
     if (status) return status;
@@ -599,9 +929,9 @@ struct Flattener {
 
 }  // namespace
 
-int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err) {
+int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err, const FlattenOptions& opt) {
   out = HostScene{};
-  Flattener f(desc, out, err);
+  Flattener f(desc, out, err, opt);
   return f.run();
 }
 

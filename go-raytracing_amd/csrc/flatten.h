@@ -16,11 +16,14 @@ struct HostScene {
   std::vector<int32_t> ref_top;       // per ref: top-level hittable index
   std::vector<DSphere> spheres;
   std::vector<int32_t> sphere_hidx;
+  std::vector<int32_t> sphere_rank;   // per prim: DFS rank inside its BLAS (tie rule)
   std::vector<DQuad> quads;
   std::vector<int32_t> quad_hidx;
+  std::vector<int32_t> quad_rank;
   std::vector<DTri> tris;
   std::vector<DTriAux> tri_aux;
   std::vector<int32_t> tri_hidx;
+  std::vector<int32_t> tri_rank;
   std::vector<DPlane> planes;
   std::vector<int32_t> plane_hidx;
   std::vector<DInstance> instances;
@@ -39,8 +42,20 @@ struct HostScene {
   int tlas_depth = 0, blas_depth = 0;
 };
 
+// How mesh BLASes are laid out (rt_ctx_set_option RT_OPT_BLAS_BUILDER).
+enum : int {
+  BLAS_REFERENCE = 0,   // the caller's BVH topology (NewBVHNode, bvh.go:69-217)
+  BLAS_SAH = 1,         // binned-SAH BVH2 over the same triangles (default)
+};
+struct FlattenOptions {
+  int blas_builder = BLAS_SAH;
+  int tlas_builder = BLAS_SAH;   // world BVH: SAH over the top-level objects, one per leaf
+  int sah_min_prims = 16;   // smaller all-triangle BLASes keep the reference topology
+};
+
 // Returns RT_OK or an rt_status; `err` receives a message.
-int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err);
+int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err,
+                  const FlattenOptions& opt = FlattenOptions());
 
 // fp64 -> fp32 with outward rounding (bbox lower / upper bounds).
 float round_down(double x);

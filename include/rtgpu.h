@@ -207,6 +207,22 @@ int rt_ctx_create(int device, rt_ctx** out);
 void rt_ctx_destroy(rt_ctx* ctx);
 const char* rt_last_error(const rt_ctx* ctx);
 
+/* Context options (take effect at the next rt_scene_upload).
+ *   RT_OPT_BLAS_BUILDER: how an all-triangle mesh BVH (LoadOBJ ->
+ *     NewBVHNode, obj_loader.go:109) is laid out on the device:
+ *     RT_BLAS_REFERENCE = the caller's topology node for node;
+ *     RT_BLAS_SAH (default) = binned-SAH BVH over the same triangles.
+ *     Both give the same closest hit: the tie rule uses the reference's
+ *     DFS ranks, not the device visiting order.
+ *   RT_OPT_TLAS_BUILDER: the world BVH (main.go:77 NewBVHNodeFromList):
+ *     RT_BLAS_REFERENCE = the caller's topology; RT_BLAS_SAH (default) =
+ *     SAH over the same top-level objects, one per leaf, each keeping its
+ *     DFS rank and its leaf's test count (volumes).  Scenes holding a
+ *     RotateX/RotateZ wrapper always keep the caller's topology.          */
+enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2 };
+enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1 };
+int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);
+
 /* Flatten + upload the Go object graph (copied; caller memory not retained). */
 int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene);
 

@@ -36,6 +36,9 @@ int main(int argc, char** argv) {
   opt.lucy_rings = 60;
   opt.lucy_cols = 80;
   if (argc > 3) opt.asset_dir = argv[3];
+  if (argc > 4 && atoi(argv[4]) > 0) { opt.lucy_rings = 0; opt.lucy_cols = 0; }   // full-size mesh
+  FlattenOptions fo;
+  if (argc > 5) fo.blas_builder = fo.tlas_builder = atoi(argv[5]);
   rts_scene* sc = nullptr;
   char err[512] = {0};
   if (rts_scene_create(argv[1], &opt, &sc, err, sizeof err) != 0) {
@@ -44,7 +47,7 @@ int main(int argc, char** argv) {
   }
   HostScene S;
   std::string ferr;
-  int rc = flatten_scene(rts_scene_get_desc(sc), S, ferr);
+  int rc = flatten_scene(rts_scene_get_desc(sc), S, ferr, fo);
   if (rc) {
     printf("{\"error\": \"flatten %d %s\"}\n", rc, ferr.c_str());
     return 4;

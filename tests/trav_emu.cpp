@@ -41,7 +41,8 @@ int main(int argc, char** argv) {
   d.ref_box = ptr(h.ref_box); d.spheres = ptr(h.spheres); d.quads = ptr(h.quads); d.tris = ptr(h.tris);
   d.tri_aux = ptr(h.tri_aux); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
-  d.lights = ptr(h.lights); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);
+  d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
+  d.tri_rank = ptr(h.tri_rank); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);
   d.quad_hidx = ptr(h.quad_hidx); d.tri_hidx = ptr(h.tri_hidx); d.plane_hidx = ptr(h.plane_hidx);
   d.volume_hidx = ptr(h.volume_hidx);
   d.tlas = h.tlas;
