@@ -184,8 +184,25 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
       for (int x = t.x; x < t.x + t.z; ++x) px.push_back(uint32_t(y) * uint32_t(dc.width) + uint32_t(x));
   const uint32_t npix = uint32_t(px.size());
   const uint32_t spp = uint32_t(p->samples_per_pixel);
-  const size_t target = size_t(4) << 20;   // path slots per batch
-  uint32_t spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
+  // Path slots per batch: as many as fit in a quarter of the free HBM, up to
+  // 128M (larger batches amortise each launch's ramp-down tail; measured on
+  // CornellBoxLucy: 4M slots 330, 64M slots 444 Msamples/s).  Samples are
+  // split evenly over the batches.  RTGPU_SLOTS overrides (tuning knob).
+  constexpr size_t kSlotBytes = 11 * sizeof(float4) + 3 * sizeof(uint32_t);
+  static const size_t env_slots = [] {
+    const char* e = getenv("RTGPU_SLOTS");
+    return e && atol(e) > 0 ? size_t(atol(e)) : size_t(0);
+  }();
+  size_t target = env_slots;
+  if (!target) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = size_t(8) << 30;
+    free_b += ctx->wslots * kSlotBytes;   // the current batch buffers can be reused
+    target = std::min<size_t>(size_t(128) << 20, std::max<size_t>(size_t(1) << 20, free_b / 4 / kSlotBytes));
+  }
+  const uint32_t max_spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
+  const uint32_t nbatch = (spp + max_spb - 1) / max_spb;
+  const uint32_t spb = (spp + nbatch - 1) / nbatch;
   const size_t nslots = size_t(spb) * npix;
   int rc;
   if (ctx->wslots < nslots) {
@@ -480,6 +497,9 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_lights = int(h.lights.size());
   d.stack_needed = h.stack_needed;
   d.has_volumes = h.volumes.empty() ? 0 : 1;
+  d.has_fancy = 0;
+  for (const DMaterial& m : h.materials)
+    if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
   ctx->has_scene = true;
   return RT_OK;
 }

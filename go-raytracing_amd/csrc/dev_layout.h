@@ -199,6 +199,7 @@ struct DScene {
   int32_t num_lights;
   int32_t stack_needed;
   int32_t has_volumes;
+  int32_t has_fancy;      // a Metal / Dielectric / Isotropic material exists
 };
 
 struct DCamera {

@@ -171,7 +171,9 @@ __global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uin
 }
 
 // ---------------------------------------------------------------- shade
-template <bool kCount>
+// kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
+// compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
+template <bool kCount, bool kEnvIS, bool kFancy>
 __global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs a, const uint32_t* q,
                                                const uint32_t* count, uint32_t* nq, uint32_t* ncount) {
   const uint32_t n = *count;
@@ -227,6 +229,8 @@ __global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs 
           if (near_zero(sd)) sd = rec.N;
           att = tex_value(sc, m.tex, rec.P);
           use_mis = sc.num_lights > 0;
+        } else if (!kFancy) {
+          scat = false;                                           // unreachable: no such material
         } else if (m.kind == 2) {                                 // Metal material.go:113-119
           V3 refl = reflect(rd, rec.N);
           refl = add(unit(refl), scale(random_unit_vector(key, bounce, DOM_SCATTER, 0), m.fuzz));
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs 
             V3 ch = mk(0.0f, 0.0f, 0.0f), ca = mk(0.0f, 0.0f, 0.0f), dh = mk(0.0f, 0.0f, 0.0f),
                da = mk(0.0f, 0.0f, 0.0f);
             float tmax_a = 0.0f;
-            if (sc.env.valid && sc.env.use_is) {                  // sampleHDRILight camera.go:565-607
+            if (kEnvIS && sc.env.valid && sc.env.use_is) {        // sampleHDRILight camera.go:565-607
               const DEnv& e = sc.env;
               V3 ldir, em;
               float pdfH;
@@ -472,7 +476,7 @@ static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
   return hipEventRecord(plan.events[n++], st);
 }
 
-template <int STACK, bool kCount, bool kVol>
+template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
   const int cus = plan.num_cus;
   hipError_t e;
@@ -484,7 +488,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
                        nslots, plan.sample_offset + s0);
     if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
     const int gext = grid_for((const void*)k_extend<STACK, kCount, kVol>, 256, 0, nslots, cus);
-    const int gsh = grid_for((const void*)k_shade<kCount>, 256, 0, nslots, cus);
+    const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy>, 256, 0, nslots, cus);
     const int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol>, 256, 0, nslots, cus);
     for (int b = 0; b < plan.max_depth; ++b) {
       uint32_t* cq = (b & 1) ? a.q1 : a.q0;
@@ -495,7 +499,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
       hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, cq, cc, nc, a.shcount,
                          a.counts + 3, a.counts + 4);
       if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_shade<kCount>), dim3(gsh), dim3(256), 0, st, sc, cam, a, cq, cc, nq, nc);
+      hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy>), dim3(gsh), dim3(256), 0, st, sc, cam, a, cq, cc, nq, nc);
       if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol>), dim3(gsd), dim3(256), 0, st, sc, a, a.counts + 4,
                          a.counts + 3);
@@ -522,7 +526,17 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
   if ((e = hipMemsetAsync(a.acc, 0, size_t(a.npix) * 3 * sizeof(double), st)) != hipSuccess) return e;
   if (plan.max_depth > 0) {
     const bool vol = sc.has_volumes != 0;
-#define RUN(S, C, V) e = run_batches<S, C, V>(sc, cam, a, plan, st)
+#define RUN(S, C, V)                                                              \
+  do {                                                                            \
+    if (envis) {                                                                  \
+      if (fancy) e = run_batches<S, C, V, true, true>(sc, cam, a, plan, st);      \
+      else e = run_batches<S, C, V, true, false>(sc, cam, a, plan, st);           \
+    } else {                                                                      \
+      if (fancy) e = run_batches<S, C, V, false, true>(sc, cam, a, plan, st);     \
+      else e = run_batches<S, C, V, false, false>(sc, cam, a, plan, st);          \
+    }                                                                             \
+  } while (0)
+    const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0;
     if (stack <= 32) {
       if (vol) { if (count) RUN(32, true, true); else RUN(32, false, true); }
       else { if (count) RUN(32, true, false); else RUN(32, false, false); }

@@ -4,7 +4,7 @@
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-count --spp 16}
+ARGS=${ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-count --spp 20}
 mkdir -p $OUT
 run() {
   name=$1; shift
@@ -14,5 +14,5 @@ run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_A
 run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD
 run tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
 run tcp TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum
-run fetch FETCH_SIZE
-run write WRITE_SIZE
+
+

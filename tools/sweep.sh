@@ -1,6 +1,8 @@
 #!/bin/bash
-# quick A/B of runtime knobs on a reduced Lucy frame
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-count --spp 100"
-for r in 4 8 16 32 48; do
-  echo -n "refill=$r "; RTGPU_REFILL=$r timeout -k 10 120 python bench.py $ARGS 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])"
+# Throughput sweep of a runtime knob (env var) on the default bench workload.
+# usage: tools/sweep.sh VAR v1 v2 ...
+VAR=$1; shift
+for v in "$@"; do
+  env $VAR=$v timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count > gpurun_out/sweep_$v.json 2>/dev/null || exit 1
+  python3 -c "import json;d=json.load(open('gpurun_out/sweep_$v.json'));print('$VAR=$v',d['value'],d['ms_per_step'])"
 done
