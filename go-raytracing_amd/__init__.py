@@ -22,7 +22,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(PKG_DIR, "lib")
+# RTGPU_LIB_DIR: an alternative in-tree build (A/B experiments), e.g. lib_w5
+LIB_DIR = os.path.join(PKG_DIR, os.environ.get("RTGPU_LIB_DIR", "lib"))
 REPO_DIR = os.path.dirname(PKG_DIR)
 ASSET_DIR = os.path.join(REPO_DIR, "assets")
 

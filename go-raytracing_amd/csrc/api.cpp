@@ -43,7 +43,7 @@ struct rt_ctx {
   hipEvent_t kev0 = nullptr, kev1 = nullptr;   // render kernel only
   bool kev_recorded = false;
   // wavefront state
-  DevBuf wstate, wq, wpix, wacc;
+  DevBuf wstate, wq, wpix, wacc, wspill;
   size_t wslots = 0;
   uint32_t* probe_pinned = nullptr;
   int num_cus = 0;
@@ -274,7 +274,14 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     plan.max_events = int(ctx->tev.size());
     plan.num_events = &ctx->tev_used;
   }
-  const int stack = ctx->host.stack_needed <= 32 ? 32 : 64;
+  // LDS stack ring (16 or 32 entries per lane, RTGPU_STACK) + global spill
+  // up to kStackMax: scenes of any supported depth run with the small ring.
+  static const int lds_stack = [] { const char* e = getenv("RTGPU_STACK"); return e && atoi(e) == 32 ? 32 : 16; }();
+  const int stack = lds_stack;
+  a.spill_lanes = uint32_t(std::max(1, ctx->num_cus)) * kSpillLanesPerCU;
+  a.spill_cap = kStackMax - stack;
+  if ((rc = ensure(ctx, ctx->wspill, size_t(a.spill_lanes) * size_t(a.spill_cap) * sizeof(uint32_t)))) return rc;
+  a.spill = static_cast<uint32_t*>(ctx->wspill.p);
   if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(hipEventRecord(ctx->kev0, st));
   HIPCHK(launch_wavefront(ctx->dscene, dc, a, plan, stack, count, d_out, p->accumulate ? 1 : 0, st));
@@ -415,6 +422,7 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   if (ctx->tiles_pinned) (void)hipHostFree(ctx->tiles_pinned);
   (void)hipEventDestroy(ctx->tiles_ev);
   free_buf(ctx->wstate); free_buf(ctx->wq); free_buf(ctx->wpix); free_buf(ctx->wacc);
+  free_buf(ctx->wspill);
   if (ctx->pix_pinned) (void)hipHostFree(ctx->pix_pinned);
   if (ctx->probe_pinned) (void)hipHostFree(ctx->probe_pinned);
   (void)hipEventDestroy(ctx->pix_ev);
@@ -495,6 +503,8 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.env.total_power = h.env_total_power;
   d.num_planes = int(h.planes.size());
   d.num_lights = int(h.lights.size());
+  d.num_materials = int(h.materials.size());
+  d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed;
   d.has_volumes = h.volumes.empty() ? 0 : 1;
   d.has_fancy = 0;

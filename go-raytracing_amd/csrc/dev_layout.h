@@ -197,6 +197,8 @@ struct DScene {
   DEnv env;
   int32_t num_planes;
   int32_t num_lights;
+  int32_t num_materials;
+  int32_t num_textures;
   int32_t stack_needed;
   int32_t has_volumes;
   int32_t has_fancy;      // a Metal / Dielectric / Isotropic material exists

@@ -373,6 +373,34 @@ __device__ bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, f
 constexpr uint32_t ITEM_NONE = 0xFFFFFFFFu;
 constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the stack"
 
+// Per-lane traversal stack: a ring of `cap` (power of two) entries in LDS,
+// entry i in slot i & (cap-1).  Pushing past `cap` moves the oldest entry of
+// the reused slot to this lane's spill area in global memory (`spill_cap`
+// more entries, rarely touched); popping below that depth brings it back.
+// Deep BVHs therefore cost LDS only for the top of the stack.
+struct TStack {
+  uint32_t* lds;       // this lane's slot 0
+  int stride;          // LDS words between slots (lanes interleaved)
+  int cap;             // LDS entries (power of two)
+  uint32_t* spill;     // this lane's spill entry 0 (nullptr: spill_cap == 0)
+  int sstride;         // words between spill entries
+  int spill_cap;
+  __device__ __forceinline__ void push(int sp, uint32_t v) const {
+    uint32_t* slot = lds + (sp & (cap - 1)) * stride;
+    if (sp >= cap) spill[(sp - cap) * sstride] = *slot;
+    *slot = v;
+  }
+  __device__ __forceinline__ uint32_t pop(int sp) const {   // sp = new depth
+    uint32_t* slot = lds + (sp & (cap - 1)) * stride;
+    const uint32_t v = *slot;
+    if (sp >= cap) *slot = spill[(sp - cap) * sstride];
+    return v;
+  }
+};
+__device__ __forceinline__ TStack lds_stack_only(uint32_t* lds, int stride, int cap) {
+  return TStack{lds, stride, cap, nullptr, 0, 0};
+}
+
 // Resumable traversal state (one lane, one ray).
 struct Trav {
   V3 wo, wd, winv;       // world-space ray (instances / volumes / restore)
@@ -428,13 +456,12 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, V3 wo, V3 wd
 //   kAny = false: closest hit in [tmin, tmax) with the tie rule.
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
 template <bool kAny, bool kCount, bool kVol>
-__device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* stk, int stride, int cap, Cnt& cnt,
-                                         int* err) {
+__device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
   Best& best = T.best;
-  auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return stk[T.sp * stride]; };
+  auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return S.pop(T.sp); };
   auto push = [&](uint32_t v) -> bool {
-    if (T.sp >= cap) { *err = 1; return false; }
-    stk[T.sp * stride] = v; ++T.sp; return true;
+    if (T.sp >= S.cap + S.spill_cap) { *err = 1; return false; }
+    S.push(T.sp, v); ++T.sp; return true;
   };
   auto postpone = [&]() {
     T.lf = T.item;
@@ -550,11 +577,11 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, uint32_t* st
 // Whole-ray traversal (probe kernel, megakernel).
 template <bool kAny, bool kCount, bool kVol = true>
 __device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin, float tmax,
-                         uint32_t* stk, int stride, int cap, Best& best, uint32_t key,
+                         const TStack& S, Best& best, uint32_t key,
                          uint32_t bounce, uint32_t voldom, Cnt& cnt, int* err) {
   Trav T;
   int s = trav_init<kAny, kCount>(sc, T, wo, wd, time, tmin, tmax, key, bounce, voldom, cnt);
-  while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol>(sc, T, stk, stride, cap, cnt, err);
+  while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol>(sc, T, S, cnt, err);
   best = T.best;
   if (kAny) return s == TRAV_ANYHIT;
   return best.kind != 0;
@@ -701,7 +728,7 @@ __device__ float env_pdf(const DEnv& e, V3 dir) {          // hdri.go:262-297
 // ----------------------------------------------------------------------------
 template <bool kCount>
 __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, uint32_t key, int depth,
-                         uint32_t* stk, int stride, int cap, Cnt& cnt, int* err) {
+                         const TStack& S, Cnt& cnt, int* err) {
   // GetRay camera.go:368-388
   float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
   float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
@@ -725,7 +752,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
   for (int dleft = depth; dleft > 0; --dleft, ++bounce) {
     Best b;
     if (kCount) cnt.rays++;
-    bool hit = traverse<false, kCount>(sc, ro, rd, time, 0.001f, __builtin_inff(), stk, stride, cap, b, key,
+    bool hit = traverse<false, kCount>(sc, ro, rd, time, 0.001f, __builtin_inff(), S, b, key,
                                        bounce, DOM_VOL, cnt, err);
     if (!hit) {                                               // camera.go:451-466
       V3 bg;
@@ -814,7 +841,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
         if (cth > 0.0f) {
           Best sb;
           if (kCount) cnt.shadow++;
-          bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, __builtin_inff(), stk, stride, cap,
+          bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, __builtin_inff(), S,
                                                 sb, key, bounce, DOM_VOL_SH_HDRI, cnt, err);
           if (!blocked) {
             float c2 = dot(rec.N, ldir);
@@ -837,7 +864,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
           if (cth > 0.0f) {
             Best sb;
             if (kCount) cnt.shadow++;
-            bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, dist - 0.001f, stk, stride, cap,
+            bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, dist - 0.001f, S,
                                                   sb, key, bounce, DOM_VOL_SH_AREA, cnt, err);
             if (!blocked) {
               const DMaterial& lm = sc.materials[lt.mat];

@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256) void render_kernel(DScene sc, DCamera cam, Ren
     double sx = 0.0, sy = 0.0, sz = 0.0;
     for (int s = s0; s < s1; ++s) {
       uint32_t key = path_key(w.seed, pix, uint32_t(w.sample_offset + s));
-      V3 L = trace_path<kCount>(sc, cam, px, py, key, w.max_depth, lds_stack + tid, 256, STACK, cnt, w.err);
+      V3 L = trace_path<kCount>(sc, cam, px, py, key, w.max_depth, lds_stack_only(lds_stack + tid, 256, STACK), cnt,
+                                   w.err);
       sx += double(L.x); sy += double(L.y); sz += double(L.z);
     }
     if (!kCount) {
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, ui
   V3 rd = sub(ps, ro);
   Best b;
   Cnt cnt = {};
-  bool hit = traverse<false, false>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack + tid, 256, STACK, b, key,
+  bool hit = traverse<false, false>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack_only(lds_stack + tid, 256, STACK), b, key,
                                     0, DOM_VOL, cnt, err);
   int top = -1, prim = -1;
   if (hit) {

@@ -32,7 +32,15 @@ struct WaveArgs {
   unsigned long long* counters;
   int* err;
   int32_t refill;   // idle lanes per wave that trigger a queue fetch
+  uint32_t* spill;  // traversal-stack spill area: spill_cap entries x spill_lanes
+  uint32_t spill_lanes;
+  int32_t spill_cap;
 };
+
+// Traversal kernels: LDS stack ring of kLdsStack entries per lane, the rest
+// of the depth (up to kStackMax) spills to global memory.
+constexpr int kStackMax = 64;
+constexpr int kSpillLanesPerCU = 2048;   // max resident threads per CU
 
 struct WavePlan {
   uint32_t spp;

@@ -24,6 +24,11 @@
 #include "device_common.h"
 #include "wavefront.h"
 
+// Minimum waves per SIMD requested for the traversal kernels (register cap).
+#ifndef RTG_TRAV_WAVES
+#define RTG_TRAV_WAVES 1
+#endif
+
 namespace rtg {
 
 __device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
@@ -122,13 +127,14 @@ __device__ __forceinline__ Fetch wave_fetch(bool idle, uint32_t* ctr, uint32_t n
 
 // ---------------------------------------------------------------- extend
 template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uint32_t* q, const uint32_t* count,
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_extend(DScene sc, WaveArgs a, const uint32_t* q, const uint32_t* count,
                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* fetch,
                                                 uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[STACK * 256];
   if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
   const uint32_t n = *count;
-  uint32_t* stk = lds_stack + threadIdx.x;
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap};
   Cnt cnt = {};
   Trav T;
   uint32_t p = ITEM_NONE;
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uin
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<false, kCount, kVol>(sc, T, stk, 256, STACK, cnt, a.err);
+      const int s = trav_step<false, kCount, kVol>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING) {
         const Best& b = T.best;
         a.hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u),
@@ -173,9 +179,27 @@ __global__ __launch_bounds__(256) void k_extend(DScene sc, WaveArgs a, const uin
 // ---------------------------------------------------------------- shade
 // kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
 // compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
+constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
+
 template <bool kCount, bool kEnvIS, bool kFancy>
-__global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs a, const uint32_t* q,
+__global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs a, const uint32_t* q,
                                                const uint32_t* count, uint32_t* nq, uint32_t* ncount) {
+  // Small scene tables (materials, textures, lights) are read from LDS: they
+  // sit on every path's dependent-load chain (hit -> material -> texture,
+  // light -> light material -> texture).
+  __shared__ DMaterial s_mat[kLdsMaterials];
+  __shared__ DTexture s_tex[kLdsTextures];
+  __shared__ DLight s_light[kLdsLights];
+  DScene sc = scg;
+  if (sc.num_materials <= kLdsMaterials && sc.num_textures <= kLdsTextures && sc.num_lights <= kLdsLights) {
+    for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = scg.materials[i];
+    for (int i = threadIdx.x; i < sc.num_textures; i += blockDim.x) s_tex[i] = scg.textures[i];
+    for (int i = threadIdx.x; i < sc.num_lights; i += blockDim.x) s_light[i] = scg.lights[i];
+    __syncthreads();
+    sc.materials = s_mat;
+    sc.textures = s_tex;
+    sc.lights = s_light;
+  }
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   Cnt cnt = {};
@@ -360,11 +384,12 @@ __global__ __launch_bounds__(256) void k_shade(DScene sc, DCamera cam, WaveArgs 
 // the visible contributions are summed in that order (camera.go:549-558) and
 // added once: L += beta_at_bounce * direct.
 template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256) void k_shadow(DScene sc, WaveArgs a, uint32_t* fetch, uint32_t* zero_c) {
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_shadow(DScene sc, WaveArgs a, uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[STACK * 256];
   if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
   const uint32_t n = *a.shcount;
-  uint32_t* stk = lds_stack + threadIdx.x;
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap};
   Cnt cnt = {};
   Trav T;
   uint32_t p = ITEM_NONE, flags = 0, key = 0, bounce = 0;
@@ -419,7 +444,7 @@ __global__ __launch_bounds__(256) void k_shadow(DScene sc, WaveArgs a, uint32_t*
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<true, kCount, kVol>(sc, T, stk, 256, STACK, cnt, a.err);
+      const int s = trav_step<true, kCount, kVol>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING && finish_ray(s)) p = ITEM_NONE;
     }
   }
@@ -487,9 +512,12 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
     hipLaunchKernelGGL(k_camera, dim3(grid_for((const void*)k_camera, 256, 0, nslots, cus)), dim3(256), 0, st, cam, a,
                        nslots, plan.sample_offset + s0);
     if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
-    const int gext = grid_for((const void*)k_extend<STACK, kCount, kVol>, 256, 0, nslots, cus);
+    const int max_trav_blocks = int(a.spill_lanes / 256u);   // one spill column per resident lane
+    int gext = grid_for((const void*)k_extend<STACK, kCount, kVol>, 256, 0, nslots, cus);
+    gext = gext < max_trav_blocks ? gext : max_trav_blocks;
     const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy>, 256, 0, nslots, cus);
-    const int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol>, 256, 0, nslots, cus);
+    int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol>, 256, 0, nslots, cus);
+    gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;
     for (int b = 0; b < plan.max_depth; ++b) {
       uint32_t* cq = (b & 1) ? a.q1 : a.q0;
       uint32_t* nq = (b & 1) ? a.q0 : a.q1;
@@ -537,12 +565,12 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     }                                                                             \
   } while (0)
     const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0;
-    if (stack <= 32) {
+    if (stack <= 16) {
+      if (vol) { if (count) RUN(16, true, true); else RUN(16, false, true); }
+      else { if (count) RUN(16, true, false); else RUN(16, false, false); }
+    } else {
       if (vol) { if (count) RUN(32, true, true); else RUN(32, false, true); }
       else { if (count) RUN(32, true, false); else RUN(32, false, false); }
-    } else {
-      if (vol) { if (count) RUN(64, true, true); else RUN(64, false, true); }
-      else { if (count) RUN(64, true, false); else RUN(64, false, false); }
     }
 #undef RUN
     if (e != hipSuccess) return e;

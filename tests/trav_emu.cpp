@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
   d.env.texels = ptr(h.env_texels); d.env.pdf = ptr(h.env_pdf); d.env.marginal = ptr(h.env_marginal);
   d.env.conditional = ptr(h.env_conditional);
   d.num_planes = int(h.planes.size()); d.num_lights = int(h.lights.size());
+  d.num_materials = int(h.materials.size()); d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed; d.has_volumes = h.volumes.empty() ? 0 : 1;
 
   const rt_camera_desc* c = rts_scene_get_camera(scn);
@@ -66,7 +67,12 @@ int main(int argc, char** argv) {
   cam.width = c->image_width; cam.height = c->image_height;
 
   const int W = cam.width, H = cam.height, cap = h.stack_needed;
-  std::vector<uint32_t> stack(static_cast<size_t>(cap));   // exactly the bound: overflow -> err, ASan sees OOB
+  // a 4-entry LDS ring + a spill area of exactly the remaining bound: every
+  // traversal deeper than 4 goes through the spill path; overflow -> err,
+  // ASan sees any out-of-range slot
+  const int ring = 4, spill_cap = cap > ring ? cap - ring : 0;
+  std::vector<uint32_t> ring_mem(static_cast<size_t>(ring)), spill_mem(static_cast<size_t>(spill_cap > 0 ? spill_cap : 1));
+  const TStack S{ring_mem.data(), 1, ring, spill_mem.data(), 1, spill_cap};
   std::vector<float> out(size_t(W) * H * 3, 0.0f);
   int e = 0;
   for (int y = 0; y < H; ++y)
@@ -75,7 +81,7 @@ int main(int argc, char** argv) {
       for (int k = 0; k < spp; ++k) {
         Cnt cnt{};
         const uint32_t key = path_key(seed, uint32_t(y * W + x), uint32_t(k));
-        V3 L = trace_path<false>(d, cam, x, y, key, c->max_depth, stack.data(), 1, cap, cnt, &e);
+        V3 L = trace_path<false>(d, cam, x, y, key, c->max_depth, S, cnt, &e);
         s[0] += L.x; s[1] += L.y; s[2] += L.z;
       }
       float* o = &out[(size_t(y) * W + x) * 3];
