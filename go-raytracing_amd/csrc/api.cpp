@@ -188,7 +188,10 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // 128M (larger batches amortise each launch's ramp-down tail; measured on
   // CornellBoxLucy: 4M slots 330, 64M slots 444 Msamples/s).  Samples are
   // split evenly over the batches.  RTGPU_SLOTS overrides (tuning knob).
-  constexpr size_t kSlotBytes = 11 * sizeof(float4) + 3 * sizeof(uint32_t);
+  // Per slot: two path streams (4 x 16 B each), hit, Lout, six NEE job
+  // fields (16 B each), job info + visibility words.
+  constexpr size_t kSlotF4 = 16;
+  constexpr size_t kSlotBytes = kSlotF4 * sizeof(float4) + 2 * sizeof(uint32_t);
   static const size_t env_slots = [] {
     const char* e = getenv("RTGPU_SLOTS");
     return e && atol(e) > 0 ? size_t(atol(e)) : size_t(0);
@@ -208,8 +211,9 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   if (ctx->wslots < nslots) {
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
-    if ((rc = ensure(ctx, ctx->wstate, nslots * 11 * sizeof(float4)))) return rc;
-    if ((rc = ensure(ctx, ctx->wq, nslots * 3 * sizeof(uint32_t) + 64))) return rc;
+    ctx->wslots = 0;
+    if ((rc = ensure(ctx, ctx->wstate, nslots * kSlotF4 * sizeof(float4)))) return rc;
+    if ((rc = ensure(ctx, ctx->wq, nslots * 2 * sizeof(uint32_t) + CNT_WORDS_Q * sizeof(uint32_t)))) return rc;
     ctx->wslots = nslots;
   }
   if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
@@ -233,15 +237,17 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   WaveArgs a{};
   float4* base = static_cast<float4*>(ctx->wstate.p);
   const size_t S = ctx->wslots;
-  a.ray_o = base; a.ray_d = base + S; a.beta = base + 2 * S; a.L = base + 3 * S; a.hit = base + 4 * S;
-  a.sh_p = base + 5 * S; a.sh_da = base + 6 * S; a.sh_dh = base + 7 * S; a.pend_a = base + 8 * S;
-  a.pend_h = base + 9 * S; a.pbeta = base + 10 * S;
+  for (int k = 0; k < 2; ++k) {
+    float4* sb = base + size_t(4 * k) * S;
+    a.s[k] = PathStream{sb, sb + S, sb + 2 * S, sb + 3 * S};
+  }
+  a.hit = base + 8 * S; a.Lout = base + 9 * S;
+  a.sj_p = base + 10 * S; a.sj_a = base + 11 * S; a.sj_h = base + 12 * S;
+  a.ne_a = base + 13 * S; a.ne_h = base + 14 * S; a.ne_beta = base + 15 * S;
   uint32_t* qb = static_cast<uint32_t*>(ctx->wq.p);
   a.counts = qb;
-  a.shcount = qb + 2;
-  a.q0 = qb + 16;
-  a.q1 = a.q0 + S;
-  a.shq = a.q1 + S;
+  a.sj_info = qb + CNT_WORDS_Q;
+  a.sj_vis = a.sj_info + S;
   a.pixels = static_cast<const uint32_t*>(ctx->wpix.p);
   a.npix = npix;
   a.acc = static_cast<double*>(ctx->wacc.p);

@@ -6,24 +6,30 @@
 
 namespace rtg {
 
-// Path-slot state, SoA of 16-B records (one dwordx4 per lane per array).
-struct WaveArgs {
-  float4* ray_o;    // o.xyz, time
-  float4* ray_d;    // d.xyz, RNG path key
+// Per-bounce path stream: one dense record per live path, indexed by its
+// position in this bounce's stream (SoA of 16-B fields, one dwordx4 per lane
+// per array, so every kernel reads and writes it coalesced).
+struct PathStream {
+  float4* o;        // ray origin.xyz, time
+  float4* d;        // ray direction.xyz, RNG path key
   float4* beta;     // throughput.xyz, state (depth_left | bounce<<16 | allow<<31)
-  float4* L;        // radiance.xyz
-  float4* hit;      // t, kind<<28|idx (0 = miss), instance, -
-  float4* sh_p;     // NEE shadow origin.xyz, flags | bounce<<8
-  float4* sh_da;    // area-light shadow dir.xyz, tmax
-  float4* sh_dh;    // HDRI shadow dir.xyz
-  float4* pend_a;   // area-light contribution if visible
-  float4* pend_h;   // HDRI contribution if visible
-  float4* pbeta;    // throughput at the NEE bounce
-  uint32_t* q0;     // extension queues (ping-pong)
-  uint32_t* q1;
-  uint32_t* shq;    // shadow queue
-  uint32_t* counts; // [0],[1] extension counts, [2] shadow count
-  uint32_t* shcount;
+  float4* L;        // radiance.xyz, path slot (sample_in_batch * npix + pixel_in_list)
+};
+
+struct WaveArgs {
+  PathStream s[2];  // ping-pong: bounce b reads s[b&1], writes survivors to s[(b&1)^1]
+  float4* hit;      // per stream position: t, kind<<28|idx (0 = miss), instance, -
+  float4* Lout;     // per path slot: final radiance.xyz (written when the path ends)
+  // NEE shadow jobs (one per path that samples a light at this bounce), dense
+  float4* sj_p;     // shadow origin.xyz, RNG path key
+  float4* sj_a;     // area-light shadow dir.xyz, tmax
+  float4* sj_h;     // HDRI shadow dir.xyz, -
+  uint32_t* sj_info;  // flags (1 area ray, 2 HDRI ray) | bounce << 8
+  uint32_t* sj_vis;   // written by k_shadow: bit r set = ray r unoccluded
+  float4* ne_a;     // area-light contribution if visible .xyz, L target
+  float4* ne_h;     // HDRI contribution if visible .xyz
+  float4* ne_beta;  // throughput at the NEE bounce .xyz
+  uint32_t* counts; // queue counters, one 128-B line each (CNT_* below)
   const uint32_t* pixels;   // pixel list (y*W + x) of this call's buckets
   uint32_t npix;
   double* acc;      // per listed pixel fp64 sums
@@ -31,11 +37,19 @@ struct WaveArgs {
   int32_t max_depth;
   unsigned long long* counters;
   int* err;
-  int32_t refill;   // idle lanes per wave that trigger a queue fetch
+  int32_t refill;   // lanes per wave lacking a prefetched item that trigger a claim
   uint32_t* spill;  // traversal-stack spill area: spill_cap entries x spill_lanes
   uint32_t spill_lanes;
   int32_t spill_cap;
 };
+
+// L target of a NEE record: the survivor's next-stream position, or the
+// path slot (bit 31) when the path ends at this bounce.
+constexpr uint32_t TARGET_SLOT = 0x80000000u;
+
+// Queue counters, each on its own 128-B line (same-line atomics serialise).
+enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT = 96, CNT_FETCH_SH = 128,
+             CNT_WORDS_Q = 160 };
 
 // Traversal kernels: LDS stack ring of kLdsStack entries per lane, the rest
 // of the depth (up to kStackMax) spills to global memory.

@@ -1,20 +1,21 @@
 // wavefront.hip — the production render path: a wavefront pipeline over
-// compacted ray queues (the north-star structure), restating the same
-// reference functions as device_common.h (camera.go:368-678 et al.).
+// dense per-bounce path streams (the north-star structure), restating the
+// same reference functions as device_common.h (camera.go:368-678 et al.).
 //
 // Per batch of path slots (slot = sample_in_batch * npix + pixel_in_list):
-//   k_camera  : GetRay (camera.go:368-388) for every slot -> extension queue
-//   repeat max_depth times:
-//     k_extend  : closest hit (BVHNode.Hit ... bvh.go:219-239) per queued ray;
-//                 minimal live state -> high occupancy for the
-//                 latency-bound traversal
-//     k_shade   : miss colour / Emitted / Scatter / sampleLightMIS set-up
-//                 (camera.go:443-518, 538-678); survivors are appended to
-//                 the next extension queue, NEE shadow rays to the shadow
-//                 queue — wave ballot + mbcnt prefix, one atomic per wave
-//     k_shadow  : any-hit shadow rays (camera.go:582, 639); adds the MIS
-//                 contribution of visible lights to the path radiance
-//   k_accum   : per-pixel fp64 sum of the batch's samples in slot order
+//   k_camera    : GetRay (camera.go:368-388) for every slot -> stream 0
+//   repeat max_depth times (stream s = bounce & 1):
+//     k_extend    : closest hit (BVHNode.Hit ... bvh.go:219-239) for every
+//                   path of stream s; persistent waves claim runs of stream
+//                   positions (one atomic per run) and prefetch the next ray
+//     k_shade     : miss colour / Emitted / Scatter / sampleLightMIS set-up
+//                   (camera.go:443-518, 538-678); survivors are written
+//                   densely to stream s^1, NEE shadow jobs densely to the job
+//                   arrays, ended paths to Lout[slot] — positions from one
+//                   block-wide prefix + one atomic per queue per block
+//     k_shadow    : any-hit shadow rays (camera.go:582, 639) -> visibility
+//     k_nee_apply : L += beta * (visible MIS contributions) (camera.go:549-558)
+//   k_accum     : per-pixel fp64 sum of the batch's samples in slot order
 // Results equal the megakernel/oracle op-for-op (same counters, same adds in
 // the same order); only the per-pixel fp64 summation grouping differs.
 #include <hip/hip_runtime.h>
@@ -39,19 +40,8 @@ __device__ __forceinline__ uint32_t pack_state(int depth, uint32_t bounce, bool 
   return uint32_t(depth & 0xFFFF) | ((bounce & 0x7FFFu) << 16) | (allow ? 0x80000000u : 0u);
 }
 
-// Append `p` to a queue when `pred`: one atomic per wave (ballot + mbcnt).
-__device__ __forceinline__ void wave_push(bool pred, uint32_t p, uint32_t* q, uint32_t* count) {
-  const unsigned long long m = __ballot(pred);
-  if (m == 0ull) return;
-  const int lane = __lane_id();
-  const int leader = __ffsll(m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(count, uint32_t(__popcll(m)));
-  base = __shfl(base, leader);
-  if (pred) {
-    const uint32_t rank = uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
-    q[base + rank] = p;
-  }
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+  return uint32_t(__popcll(m & ((1ull << __lane_id()) - 1ull)));
 }
 
 __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n, uint32_t samples) {
@@ -71,13 +61,14 @@ __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n
 }
 
 // ---------------------------------------------------------------- camera
-__global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, uint32_t nslots, uint32_t sample_base) {
+__global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, PathStream s, uint32_t nslots,
+                                                uint32_t sample_base) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += gs) {
-    const uint32_t s = i / a.npix, pi = i - s * a.npix;
+    const uint32_t sm = i / a.npix, pi = i - sm * a.npix;
     const uint32_t pix = a.pixels[pi];
     const int px = int(pix % uint32_t(cam.width)), py = int(pix / uint32_t(cam.width));
-    const uint32_t key = path_key(a.seed, pix, sample_base + s);
+    const uint32_t key = path_key(a.seed, pix, sample_base + sm);
     // GetRay camera.go:368-388
     float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
     float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
@@ -94,102 +85,140 @@ __global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, uint32_
       ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
     }
     V3 rd = sub(ps, ro);
-    a.ray_o[i] = make_float4(ro.x, ro.y, ro.z, time);
-    a.ray_d[i] = make_float4(rd.x, rd.y, rd.z, asf(key));
-    a.beta[i] = make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true)));
-    a.L[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    a.q0[i] = i;
+    s.o[i] = make_float4(ro.x, ro.y, ro.z, time);
+    s.d[i] = make_float4(rd.x, rd.y, rd.z, asf(key));
+    s.beta[i] = make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true)));
+    s.L[i] = make_float4(0.0f, 0.0f, 0.0f, asf(i));
   }
 }
 
-// ---------------------------------------------------------------- refill
-// Persistent traversal lanes: when at least kRefill lanes of a wave are idle,
-// the wave grabs that many queue entries with one atomic (ballot + mbcnt).
-
-struct Fetch {
-  uint32_t idx;      // queue index for this lane (valid if < n)
-  bool exhausted;    // wave-uniform: the queue is drained
+// ---------------------------------------------------------------- claim pool
+// Per-wave claim pool over a queue [0, n) (guided self-scheduling): a wave
+// claims a run of queue positions with one atomic and hands them to its
+// lanes without further atomics; runs shrink as the queue drains so the
+// waves finish together.  Every field is wave-uniform.
+struct Pool {
+  uint32_t cur, end;   // unhanded part of the wave's current run
+  bool dry;            // the queue is drained
 };
-__device__ __forceinline__ Fetch wave_fetch(bool idle, uint32_t* ctr, uint32_t n, int refill) {
-  Fetch f{0xFFFFFFFFu, false};
-  const unsigned long long m = __ballot(idle);
-  const int nidle = __popcll(m);
-  if (nidle < refill) return f;
-  const int lane = __lane_id();
-  const int leader = __ffsll(m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(ctr, uint32_t(nidle));
-  base = __shfl(base, leader);
-  f.exhausted = base + uint32_t(nidle) >= n;
-  if (idle) f.idx = base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
-  return f;
+
+// Called by the whole wave (converged).  Lanes with `want` get a queue
+// position (or ITEM_NONE).  A new run is claimed only when the wave's run is
+// used up and at least `refill` lanes want an item.
+__device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr, uint32_t n, uint32_t nwaves,
+                                              int refill) {
+  const unsigned long long m = __ballot(want);
+  const uint32_t nw = uint32_t(__popcll(m));
+  if (P.dry || nw == 0u) return ITEM_NONE;
+  if (P.cur >= P.end) {
+    if (nw < uint32_t(refill)) return ITEM_NONE;
+    uint32_t run = (n > P.end ? n - P.end : 0u) / (4u * nwaves);
+    run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
+    const int leader = __ffsll(m) - 1;
+    uint32_t base = 0;
+    if (__lane_id() == leader) base = atomicAdd(ctr, run);
+    base = __shfl(base, leader);
+    if (base >= n) { P.dry = true; return ITEM_NONE; }
+    P.cur = base;
+    P.end = n - base > run ? base + run : n;
+  }
+  const uint32_t avail = P.end - P.cur;
+  const uint32_t rank = lanes_below(m);
+  const uint32_t idx = (want && rank < avail) ? P.cur + rank : ITEM_NONE;
+  P.cur += nw < avail ? nw : avail;
+  return idx;
+}
+
+__device__ __forceinline__ void store_hit(float4* hit, uint32_t p, const Best& b) {
+  hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
+                       0.0f);
 }
 
 // ---------------------------------------------------------------- extend
+// Each lane holds the ray it traverses (p) and a prefetched next ray (pn):
+// the prefetch's loads are in flight while the lane traverses, so a lane
+// that finishes starts its next ray on the following step without waiting.
 template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_extend(DScene sc, WaveArgs a, const uint32_t* q, const uint32_t* count,
-                                                uint32_t* zero_a, uint32_t* zero_b, uint32_t* fetch,
-                                                uint32_t* zero_c) {
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_extend(DScene sc, WaveArgs a, PathStream cs,
+                                                                const uint32_t* count, uint32_t* zero_a,
+                                                                uint32_t* zero_b, uint32_t* zero_c, uint32_t* fetch) {
   __shared__ uint32_t lds_stack[STACK * 256];
+  // next stream's count, the shadow job count and the shadow fetch counter
   if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
   const uint32_t n = *count;
+  const uint32_t nwaves = gridDim.x * (blockDim.x / 64u);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap};
   Cnt cnt = {};
   Trav T;
-  uint32_t p = ITEM_NONE;
-  bool exhausted = false;
+  Pool P{0u, 0u, false};
+  uint32_t p = ITEM_NONE, pn = ITEM_NONE;
+  float4 po = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pd = po;
+  uint32_t pb = 0;
   for (;;) {
-    if (!exhausted) {
-      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n, a.refill);
-      exhausted = f.exhausted;
-      if (f.idx < n) {
-        p = q[f.idx];
-        const float4 o = a.ray_o[p], d = a.ray_d[p];
-        uint32_t bounce = 0;
-        if (kVol) bounce = (asu(a.beta[p].w) >> 16) & 0x7FFFu;
-        if (kCount) cnt.rays++;
-        const int s = trav_init<false, kCount>(sc, T, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), o.w, 0.001f,
-                                               __builtin_inff(), asu(d.w), bounce, DOM_VOL, cnt);
-        if (s != TRAV_RUNNING) {
-          const Best& b = T.best;
-          a.hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u),
-                                 asf(uint32_t(b.inst)), 0.0f);
-          p = ITEM_NONE;
-        }
-      }
+    if (p == ITEM_NONE && pn != ITEM_NONE) {
+      p = pn;
+      pn = ITEM_NONE;
+      if (kCount) cnt.rays++;
+      const int s = trav_init<false, kCount>(sc, T, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), po.w, 0.001f,
+                                             __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
+      if (s != TRAV_RUNNING) { store_hit(a.hit, p, T.best); p = ITEM_NONE; }
     }
-    if (!__any(p != ITEM_NONE)) {
-      if (exhausted) break;
+    const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
+    if (idx != ITEM_NONE) {
+      pn = idx;
+      po = cs.o[idx];
+      pd = cs.d[idx];
+      if (kVol) pb = (asu(cs.beta[idx].w) >> 16) & 0x7FFFu;
+    }
+    if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
+      if (P.dry) break;
       continue;
     }
     if (p != ITEM_NONE) {
       const int s = trav_step<false, kCount, kVol>(sc, T, S, cnt, a.err);
-      if (s != TRAV_RUNNING) {
-        const Best& b = T.best;
-        a.hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u),
-                               asf(uint32_t(b.inst)), 0.0f);
-        p = ITEM_NONE;
-      }
+      if (s != TRAV_RUNNING) { store_hit(a.hit, p, T.best); p = ITEM_NONE; }
     }
   }
   if (kCount) add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
 }
 
 // ---------------------------------------------------------------- shade
+// Positions in the two output queues (survivors, NEE jobs) for every thread
+// of the block: wave ballots, a block-wide prefix in LDS and one atomic per
+// queue per block.  `sw`/`sb` are this iteration's (double-buffered) slots.
+__device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, uint32_t* q1, uint32_t (*sw)[4],
+                                               uint32_t* sb, uint32_t& p0, uint32_t& p1) {
+  const unsigned long long m0 = __ballot(c0), m1 = __ballot(c1);
+  const int w = int(threadIdx.x >> 6);
+  if (__lane_id() == 0) { sw[0][w] = uint32_t(__popcll(m0)); sw[1][w] = uint32_t(__popcll(m1)); }
+  __syncthreads();
+  if (threadIdx.x < 2u) {
+    const int q = int(threadIdx.x);
+    uint32_t tot = 0;
+    for (int k = 0; k < 4; ++k) { const uint32_t c = sw[q][k]; sw[q][k] = tot; tot += c; }
+    sb[q] = tot ? atomicAdd(q ? q1 : q0, tot) : 0u;
+  }
+  __syncthreads();
+  p0 = sb[0] + sw[0][w] + lanes_below(m0);
+  p1 = sb[1] + sw[1][w] + lanes_below(m1);
+}
+
 // kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
 // compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 
 template <bool kCount, bool kEnvIS, bool kFancy>
-__global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs a, const uint32_t* q,
-                                               const uint32_t* count, uint32_t* nq, uint32_t* ncount) {
+__global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+                                               const uint32_t* count, PathStream ns, uint32_t* ncount) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
   // sit on every path's dependent-load chain (hit -> material -> texture,
   // light -> light material -> texture).
   __shared__ DMaterial s_mat[kLdsMaterials];
   __shared__ DTexture s_tex[kLdsTextures];
   __shared__ DLight s_light[kLdsLights];
+  __shared__ uint32_t s_w[2][2][4];
+  __shared__ uint32_t s_b[2][2];
   DScene sc = scg;
   if (sc.num_materials <= kLdsMaterials && sc.num_textures <= kLdsTextures && sc.num_lights <= kLdsLights) {
     for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = scg.materials[i];
@@ -203,25 +232,28 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   Cnt cnt = {};
-  // uniform trip count per wave so the ballots in wave_push see every lane
-  const uint32_t n_up = (n + 63u) & ~63u;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += gs) {
-    bool live = i < n;
+  // block-uniform trip count (blockDim 256, gs a multiple of 256): every
+  // thread reaches the block_reserve2 barriers
+  const uint32_t n_up = (n + 255u) & ~255u;
+  uint32_t par = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += gs, par ^= 1u) {
+    const bool live = i < n;
     bool cont = false, want_shadow = false;
-    uint32_t p = 0;
+    uint32_t slot = 0, key = 0, flags = 0, bounce = 0, nstate = 0;
+    float time = 0.0f, tmax_a = 0.0f;
+    V3 L = mk(0.0f, 0.0f, 0.0f), P = L, sd = L, beta = L, nbeta = L, ca = L, ch = L, da = L, dh = L;
     if (live) {
-      p = q[i];
-      const float4 h = a.hit[p], o4 = a.ray_o[p], d4 = a.ray_d[p], b4 = a.beta[p];
-      float4 L4 = a.L[p];
-      const uint32_t key = asu(d4.w);
+      const float4 h = a.hit[i], o4 = cs.o[i], d4 = cs.d[i], b4 = cs.beta[i], L4 = cs.L[i];
+      key = asu(d4.w);
+      slot = asu(L4.w);
       const uint32_t st = asu(b4.w);
       const int dleft = int(st & 0xFFFFu);
-      const uint32_t bounce = (st >> 16) & 0x7FFFu;
+      bounce = (st >> 16) & 0x7FFFu;
       const bool allow = (st >> 31) != 0u;
       const V3 ro = mk(o4.x, o4.y, o4.z), rd = mk(d4.x, d4.y, d4.z);
-      const float time = o4.w;
-      V3 beta = mk(b4.x, b4.y, b4.z);
-      V3 L = mk(L4.x, L4.y, L4.z);
+      time = o4.w;
+      beta = mk(b4.x, b4.y, b4.z);
+      L = mk(L4.x, L4.y, L4.z);
       const uint32_t kh = asu(h.y);
       if (kh == 0u) {                                            // miss (camera.go:451-466)
         V3 bg;
@@ -241,9 +273,10 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
         b.t = h.x; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = int(asu(h.z));
         b.refpos = 0; b.primpos = 0;
         Rec rec = make_record(sc, b, ro, rd, time);
+        P = rec.P;
         const DMaterial& m = sc.materials[rec.mat];
         if (kCount) cnt.mat++;
-        V3 att = mk(0.0f, 0.0f, 0.0f), sd = mk(0.0f, 0.0f, 0.0f);
+        V3 att = mk(0.0f, 0.0f, 0.0f);
         bool scat = true, use_mis = false;
         if (m.kind == 4) {                                        // DiffuseLight
           if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.P)));
@@ -286,10 +319,6 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
             const int nl = sc.num_lights;
             int li = int(rnd(key, ctr(bounce, DOM_NEE, 0)) * float(nl));
             if (li >= nl) li = nl - 1;
-            uint32_t flags = 0;
-            V3 ch = mk(0.0f, 0.0f, 0.0f), ca = mk(0.0f, 0.0f, 0.0f), dh = mk(0.0f, 0.0f, 0.0f),
-               da = mk(0.0f, 0.0f, 0.0f);
-            float tmax_a = 0.0f;
             if (kEnvIS && sc.env.valid && sc.env.use_is) {        // sampleHDRILight camera.go:565-607
               const DEnv& e = sc.env;
               V3 ldir, em;
@@ -353,102 +382,138 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
                 }
               }
             }
-            if (flags) {
-              want_shadow = true;
-              a.sh_p[p] = make_float4(rec.P.x, rec.P.y, rec.P.z, asf(flags | (bounce << 8)));
-              a.sh_da[p] = make_float4(da.x, da.y, da.z, tmax_a);
-              a.sh_dh[p] = make_float4(dh.x, dh.y, dh.z, 0.0f);
-              a.pend_a[p] = make_float4(ca.x, ca.y, ca.z, 0.0f);
-              a.pend_h[p] = make_float4(ch.x, ch.y, ch.z, 0.0f);
-              a.pbeta[p] = make_float4(beta.x, beta.y, beta.z, 0.0f);
-            }
+            want_shadow = flags != 0u;
           }
-          beta = mul(beta, att);
+          nbeta = mul(beta, att);
           const int nd = dleft - 1;
           cont = nd > 0;
-          a.ray_o[p] = make_float4(rec.P.x, rec.P.y, rec.P.z, time);
-          a.ray_d[p] = make_float4(sd.x, sd.y, sd.z, d4.w);
-          a.beta[p] = make_float4(beta.x, beta.y, beta.z, asf(pack_state(nd, bounce + 1u, !use_mis)));
+          nstate = pack_state(nd, bounce + 1u, !use_mis);
         }
       }
-      a.L[p] = make_float4(L.x, L.y, L.z, L4.w);
     }
-    wave_push(cont, p, nq, ncount);
-    wave_push(want_shadow, p, a.shq, a.shcount);
+    uint32_t jc, js;
+    block_reserve2(cont, want_shadow, ncount, a.counts + CNT_SHADOW, s_w[par], s_b[par], jc, js);
+    if (cont) {
+      ns.o[jc] = make_float4(P.x, P.y, P.z, time);
+      ns.d[jc] = make_float4(sd.x, sd.y, sd.z, asf(key));
+      ns.beta[jc] = make_float4(nbeta.x, nbeta.y, nbeta.z, asf(nstate));
+      ns.L[jc] = make_float4(L.x, L.y, L.z, asf(slot));
+    } else if (live) {
+      a.Lout[slot] = make_float4(L.x, L.y, L.z, 0.0f);
+    }
+    if (want_shadow) {
+      a.sj_p[js] = make_float4(P.x, P.y, P.z, asf(key));
+      a.sj_a[js] = make_float4(da.x, da.y, da.z, tmax_a);
+      if (kEnvIS) a.sj_h[js] = make_float4(dh.x, dh.y, dh.z, 0.0f);
+      a.sj_info[js] = flags | (bounce << 8);
+      a.ne_a[js] = make_float4(ca.x, ca.y, ca.z, asf(cont ? jc : (slot | TARGET_SLOT)));
+      if (kEnvIS) a.ne_h[js] = make_float4(ch.x, ch.y, ch.z, 0.0f);
+      a.ne_beta[js] = make_float4(beta.x, beta.y, beta.z, 0.0f);
+    }
   }
   if (kCount) add_counters(a.counters + KC_SHADE * CNT_BLOCK, cnt, 0);
 }
 
 // ---------------------------------------------------------------- shadow
 // One job = one path's NEE: HDRI ray (flag 2) then area-light ray (flag 1);
-// the visible contributions are summed in that order (camera.go:549-558) and
-// added once: L += beta_at_bounce * direct.
-template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_shadow(DScene sc, WaveArgs a, uint32_t* fetch, uint32_t* zero_c) {
+// the job's visibility bits go to sj_vis (k_nee_apply sums the visible
+// contributions in that order, camera.go:549-558).  Lanes prefetch their next
+// job as k_extend does.
+template <int STACK, bool kCount, bool kVol, bool kEnvIS>
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
+                                                                uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[STACK * 256];
   if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
-  const uint32_t n = *a.shcount;
+  const uint32_t n = *count;
+  const uint32_t nwaves = gridDim.x * (blockDim.x / 64u);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap};
   Cnt cnt = {};
   Trav T;
-  uint32_t p = ITEM_NONE, flags = 0, key = 0, bounce = 0;
+  Pool Q{0u, 0u, false};
+  uint32_t p = ITEM_NONE, pn = ITEM_NONE;
+  // current job
+  uint32_t key = 0, info = 0, vis = 0;
   int r = 0;
-  V3 P = mk(0.0f, 0.0f, 0.0f), direct = mk(0.0f, 0.0f, 0.0f);
-  bool exhausted = false;
-  // start ray `r` of the current job; returns the init status
-  auto start_ray = [&](int rr) -> int {
-    const float4 dd = rr == 0 ? a.sh_dh[p] : a.sh_da[p];
-    const float tmax = rr == 0 ? __builtin_inff() : dd.w;      // camera.go:582 / :639
+  V3 P = mk(0.0f, 0.0f, 0.0f);
+  float4 da = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  // prefetched job
+  float4 qp = da, qa = da, qh = da;
+  uint32_t qinfo = 1u;
+  auto start_ray = [&](int rr, V3 dir, float tmax) -> int {
     if (kCount) cnt.shadow++;
-    return trav_init<true, kCount>(sc, T, P, mk(dd.x, dd.y, dd.z), 0.0f, 0.001f, tmax, key, bounce,
+    return trav_init<true, kCount>(sc, T, P, dir, 0.0f, 0.001f, tmax, key, info >> 8,
                                    rr == 0 ? DOM_VOL_SH_HDRI : DOM_VOL_SH_AREA, cnt);
   };
-  // a ray finished with status s; returns true when the whole job is done
-  auto finish_ray = [&](int s) -> bool {
-    if (s != TRAV_ANYHIT) {
-      const float4 c = r == 0 ? a.pend_h[p] : a.pend_a[p];
-      direct = add(direct, mk(c.x, c.y, c.z));
-    }
-    while (r == 0 && (flags & 1u)) {
+  // ray r of the current job ended with status s; true when the job is done
+  auto advance = [&](int s) -> bool {
+    if (s != TRAV_ANYHIT) vis |= r == 0 ? 2u : 1u;
+    if (r == 0 && (info & 1u)) {
       r = 1;
-      const int s2 = start_ray(1);
+      const int s2 = start_ray(1, mk(da.x, da.y, da.z), da.w);
       if (s2 == TRAV_RUNNING) return false;
-      if (s2 != TRAV_ANYHIT) { const float4 c = a.pend_a[p]; direct = add(direct, mk(c.x, c.y, c.z)); }
+      if (s2 != TRAV_ANYHIT) vis |= 1u;
     }
-    const float4 pb = a.pbeta[p];
-    const float4 L4 = a.L[p];
-    const V3 L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
-    a.L[p] = make_float4(L.x, L.y, L.z, L4.w);
+    a.sj_vis[p] = vis;
     return true;
   };
   for (;;) {
-    if (!exhausted) {
-      const Fetch f = wave_fetch(p == ITEM_NONE, fetch, n, a.refill);
-      exhausted = f.exhausted;
-      if (f.idx < n) {
-        p = a.shq[f.idx];
-        const float4 P4 = a.sh_p[p];
-        flags = asu(P4.w) & 0xFFu;
-        bounce = asu(P4.w) >> 8;
-        key = asu(a.ray_d[p].w);
-        P = mk(P4.x, P4.y, P4.z);
-        direct = mk(0.0f, 0.0f, 0.0f);
-        r = (flags & 2u) ? 0 : 1;
-        const int s = start_ray(r);
-        if (s != TRAV_RUNNING && finish_ray(s)) p = ITEM_NONE;
+    if (p == ITEM_NONE && pn != ITEM_NONE) {
+      p = pn;
+      pn = ITEM_NONE;
+      P = mk(qp.x, qp.y, qp.z);
+      key = asu(qp.w);
+      info = qinfo;
+      da = qa;
+      vis = 0u;
+      int s;
+      if (kEnvIS && (info & 2u)) {
+        r = 0;
+        s = start_ray(0, mk(qh.x, qh.y, qh.z), __builtin_inff());   // camera.go:582
+      } else {
+        r = 1;
+        s = start_ray(1, mk(da.x, da.y, da.z), da.w);               // camera.go:639
       }
+      if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
-    if (!__any(p != ITEM_NONE)) {
-      if (exhausted) break;
+    const uint32_t idx = pool_take(pn == ITEM_NONE, Q, fetch, n, nwaves, a.refill);
+    if (idx != ITEM_NONE) {
+      pn = idx;
+      qp = a.sj_p[idx];
+      qa = a.sj_a[idx];
+      if (kEnvIS) qh = a.sj_h[idx];
+      if (kEnvIS || kVol) qinfo = a.sj_info[idx];
+    }
+    if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
+      if (Q.dry) break;
       continue;
     }
     if (p != ITEM_NONE) {
       const int s = trav_step<true, kCount, kVol>(sc, T, S, cnt, a.err);
-      if (s != TRAV_RUNNING && finish_ray(s)) p = ITEM_NONE;
+      if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
   }
   if (kCount) add_counters(a.counters + KC_SHADOW * CNT_BLOCK, cnt, 0);
+}
+
+// ---------------------------------------------------------------- NEE apply
+// L_target += beta_at_bounce * (HDRI contribution if visible + area-light
+// contribution if visible), summed in that order (camera.go:549-558).
+__global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count, float4* Lnext) {
+  const uint32_t n = *count;
+  const uint32_t gs = gridDim.x * blockDim.x;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
+    const uint32_t flags = a.sj_info[k] & 0xFFu, vis = a.sj_vis[k];
+    const float4 ea = a.ne_a[k], pb = a.ne_beta[k];
+    V3 direct = mk(0.0f, 0.0f, 0.0f);
+    if ((flags & 2u) && (vis & 2u)) { const float4 eh = a.ne_h[k]; direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+    if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
+    const uint32_t t = asu(ea.w);
+    float4* Lp = (t & TARGET_SLOT) ? a.Lout + (t & ~TARGET_SLOT) : Lnext + t;
+    const float4 L4 = *Lp;
+    const V3 L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
+    *Lp = make_float4(L.x, L.y, L.z, L4.w);
+  }
 }
 
 // ---------------------------------------------------------------- accumulate
@@ -457,7 +522,7 @@ __global__ __launch_bounds__(256) void k_accum(WaveArgs a, uint32_t nsamp) {
   for (uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x; pi < a.npix; pi += gs) {
     double sx = a.acc[size_t(pi) * 3], sy = a.acc[size_t(pi) * 3 + 1], sz = a.acc[size_t(pi) * 3 + 2];
     for (uint32_t s = 0; s < nsamp; ++s) {
-      const float4 L = a.L[size_t(s) * a.npix + pi];
+      const float4 L = a.Lout[size_t(s) * a.npix + pi];
       sx += double(L.x); sy += double(L.y); sz += double(L.z);
     }
     a.acc[size_t(pi) * 3] = sx; a.acc[size_t(pi) * 3 + 1] = sy; a.acc[size_t(pi) * 3 + 2] = sz;
@@ -475,7 +540,9 @@ __global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int ac
 }
 
 __global__ void k_set_counts(uint32_t* c, uint32_t n) {
-  if (threadIdx.x == 0) { c[0] = n; c[1] = 0u; c[2] = 0u; c[3] = 0u; c[4] = 0u; }
+  if (threadIdx.x == 0) {
+    c[CNT_STREAM0] = n; c[CNT_STREAM1] = 0u; c[CNT_SHADOW] = 0u; c[CNT_FETCH_EXT] = 0u; c[CNT_FETCH_SH] = 0u;
+  }
 }
 
 __global__ void k_count_samples(WaveArgs a, uint32_t n) {
@@ -505,37 +572,42 @@ template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
   const int cus = plan.num_cus;
   hipError_t e;
+  uint32_t* const cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
+  uint32_t* const cnt_shadow = a.counts + CNT_SHADOW;
+  uint32_t* const fetch_ext = a.counts + CNT_FETCH_EXT;
+  uint32_t* const fetch_sh = a.counts + CNT_FETCH_SH;
   for (uint32_t s0 = 0; s0 < plan.spp; s0 += plan.samples_per_batch) {
     const uint32_t sb = plan.spp - s0 < plan.samples_per_batch ? plan.spp - s0 : plan.samples_per_batch;
     const uint32_t nslots = sb * a.npix;
     hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, a.counts, nslots);
     hipLaunchKernelGGL(k_camera, dim3(grid_for((const void*)k_camera, 256, 0, nslots, cus)), dim3(256), 0, st, cam, a,
-                       nslots, plan.sample_offset + s0);
+                       a.s[0], nslots, plan.sample_offset + s0);
     if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
     const int max_trav_blocks = int(a.spill_lanes / 256u);   // one spill column per resident lane
     int gext = grid_for((const void*)k_extend<STACK, kCount, kVol>, 256, 0, nslots, cus);
     gext = gext < max_trav_blocks ? gext : max_trav_blocks;
     const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy>, 256, 0, nslots, cus);
-    int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol>, 256, 0, nslots, cus);
+    int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS>, 256, 0, nslots, cus);
     gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;
+    const int gap = grid_for((const void*)k_nee_apply, 256, 0, nslots, cus);
     for (int b = 0; b < plan.max_depth; ++b) {
-      uint32_t* cq = (b & 1) ? a.q1 : a.q0;
-      uint32_t* nq = (b & 1) ? a.q0 : a.q1;
-      uint32_t* cc = a.counts + (b & 1);
-      uint32_t* nc = a.counts + ((b & 1) ^ 1);
+      const int c = b & 1, nx = c ^ 1;
       if ((e = mark(plan, KC_EXTEND, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, cq, cc, nc, a.shcount,
-                         a.counts + 3, a.counts + 4);
+      hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, a.s[c], cnt_stream[c],
+                         cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext);
       if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy>), dim3(gsh), dim3(256), 0, st, sc, cam, a, cq, cc, nq, nc);
+      hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
+                         cnt_stream[c], a.s[nx], cnt_stream[nx]);
       if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol>), dim3(gsd), dim3(256), 0, st, sc, a, a.counts + 4,
-                         a.counts + 3);
+      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS>), dim3(gsd), dim3(256), 0, st, sc, a, cnt_shadow,
+                         fetch_sh, fetch_ext);
       if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_nee_apply, dim3(gap), dim3(256), 0, st, a, cnt_shadow, a.s[nx].L);
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
         // long-tail scenes (RandomScene depth 50): stop once every path ended
         uint32_t left = 0;
-        if ((e = hipMemcpyAsync(plan.probe_host, nc, sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        if ((e = hipMemcpyAsync(plan.probe_host, cnt_stream[nx], sizeof(uint32_t), hipMemcpyDeviceToHost, st)) !=
+            hipSuccess)
           return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
         left = *plan.probe_host;

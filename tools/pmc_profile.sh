@@ -1,10 +1,10 @@
 #!/bin/bash
 # PMC passes (one counter group per pass, never combined with tracing) of
-# bench.py on a reduced-spp CornellBoxLucy frame.  Output: gpurun_out/pmc/<pass>/
+# bench.py on the default workload (one step).  Output: gpurun_out/pmc/<pass>/
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-count --spp 20}
+ARGS=${ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-count}
 mkdir -p $OUT
 run() {
   name=$1; shift

@@ -2,8 +2,8 @@
 # Round profile of the default bench workload (one gpurun call):
 #   1. rocprofv3 --kernel-trace --stats of bench.py (per-kernel durations)
 #   2. separate --pmc passes for FETCH_SIZE and WRITE_SIZE (HBM traffic),
-#      never combined with tracing, on the same frame at 100 spp (same
-#      per-launch shape as 500 spp: 5 samples per pixel per batch)
+#      never combined with tracing, on the same workload (500 spp, one step:
+#      the same per-launch batches as the timed bench steps)
 # Outputs under gpurun_out/prof/; tools/pmc_traffic.py turns them into
 # profiles/pmc_<scene>_<W>x<H>.json.
 set -o pipefail
@@ -14,6 +14,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/k
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o p -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --spp 100 > $OUT/$c.json 2> $OUT/$c.err || exit 1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count > $OUT/$c.json 2> $OUT/$c.err || exit 1
 done
 echo done
