@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 
 # Algorithmic bytes per unit of work.
 BYTES = {
-    "node_visits": 64,       # one BVH2 node = two 32-B child boxes
+    "node_visits": 128,      # one BVH4 node = four 24-B child boxes + four child items
     "tri_tests": 36,         # v0, e1, e2 fp32
     "sphere_tests": 32,
     "quad_tests": 64,

@@ -470,7 +470,7 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   DScene& d = ctx->dscene;
   d = DScene{};
 #define UP(vec, field) if ((rc = upload_vec(ctx, h.vec, &d.field))) { free_scene(ctx); return rc; }
-  UP(nodes, nodes);
+  UP(nodes4, nodes);
   UP(leaves, leaves);
   UP(refs, refs);
   UP(ref_rank, ref_rank);
@@ -524,7 +524,7 @@ int rt_scene_get_info(const rt_ctx* ctx, rt_scene_info* o) {
   if (!ctx || !o) return RT_ERR_INVALID;
   if (!ctx->has_scene) return RT_ERR_NO_SCENE;
   const HostScene& h = ctx->host;
-  o->nodes = int(h.nodes.size());
+  o->nodes = int(h.nodes4.size());   // device BVH4 nodes
   o->leaves = int(h.leaves.size());
   o->refs = int(h.refs.size());
   o->spheres = int(h.spheres.size());

@@ -62,6 +62,17 @@ struct alignas(16) DNode {
   uint32_t pad0, pad1;
 };
 
+// BVH4 node, 128 B (one L2 line): up to four children's boxes as SoA rows
+// (lane c of each row = child c) + child items; an unused slot has an empty
+// box (lo = +inf, hi = -inf), which every slab test rejects.  Built by
+// collapsing the BVH2 above (flatten.cpp collapse_bvh4): the traversal
+// fetches half as many dependent nodes.
+struct alignas(16) DNode4 {
+  float xlo[4], xhi[4], ylo[4], yhi[4], zlo[4], zhi[4];
+  uint32_t item[4];
+  uint32_t pad[4];
+};
+
 struct alignas(8) DLeaf {
   uint32_t first;  // index into refs (PK_MIXED) or into the kind's prim array
   uint32_t info;
@@ -166,7 +177,7 @@ struct alignas(16) DRefBox {
 
 // Everything the kernels need, passed by value as a kernel argument.
 struct DScene {
-  const DNode* nodes;
+  const DNode4* nodes;         // BVH4 nodes (ITEM_NODE indexes this array)
   const DLeaf* leaves;
   const uint32_t* refs;
   const int32_t* ref_rank;     // DFS rank of each TLAS ref (tie rule)

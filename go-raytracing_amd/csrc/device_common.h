@@ -467,26 +467,37 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     T.lf = T.item;
     T.item = ((T.lf >> ITEM_SHIFT) == ITEM_LEAF) ? pop() : ITEM_POP;
   };
-  // ---------------- phase 1: internal nodes
+  // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
     const float4* np = reinterpret_cast<const float4*>(sc.nodes + (T.item & ITEM_MASK));
-    const float4 a = np[0], b = np[1], c = np[2];
-    const uint4 m = reinterpret_cast<const uint4*>(np)[3];
+    const float4 xl = np[0], xh = np[1], yl = np[2], yh = np[3], zl = np[4], zh = np[5];
+    const uint4 it = reinterpret_cast<const uint4*>(np)[6];
     if (kCount) cnt.nodes++;
     const float hi = kAny ? T.tmax : best.t;
-    float tl, tr;
-    const bool hl = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, T.cr, T.tmin, hi, tl);
-    const bool hr = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, T.cr, T.tmin, hi, tr);
-    if (hl && hr) {
-      const bool swap = tr < tl;
-      if (!push(swap ? m.x : m.y)) return TRAV_DONE;
-      T.item = swap ? m.y : m.x;
-    } else if (hl) {
-      T.item = m.x;
-    } else if (hr) {
-      T.item = m.y;
-    } else {
+    // entry distance per child, +inf when missed
+    float t0, t1, t2, t3;
+    const float inf = __builtin_inff();
+    t0 = box_hit(xl.x, xh.x, yl.x, yh.x, zl.x, zh.x, T.cr, T.tmin, hi, t0) ? t0 : inf;
+    t1 = box_hit(xl.y, xh.y, yl.y, yh.y, zl.y, zh.y, T.cr, T.tmin, hi, t1) ? t1 : inf;
+    t2 = box_hit(xl.z, xh.z, yl.z, yh.z, zl.z, zh.z, T.cr, T.tmin, hi, t2) ? t2 : inf;
+    t3 = box_hit(xl.w, xh.w, yl.w, yh.w, zl.w, zh.w, T.cr, T.tmin, hi, t3) ? t3 : inf;
+    const int nh = int(t0 < inf) + int(t1 < inf) + int(t2 < inf) + int(t3 < inf);
+    if (nh == 0) {
       T.item = pop();
+    } else {
+      // near-to-far order (5-comparator network); visit the nearest, push the
+      // other hit children far first
+      uint32_t i0 = it.x, i1 = it.y, i2 = it.z, i3 = it.w;
+      auto cs = [](float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
+        const bool sw = tb < ta;
+        const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
+        const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
+      };
+      cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2);
+      if (nh > 3 && !push(i3)) return TRAV_DONE;
+      if (nh > 2 && !push(i2)) return TRAV_DONE;
+      if (nh > 1 && !push(i1)) return TRAV_DONE;
+      T.item = i0;
     }
     // leaving an instance with nothing postponed: restore the world ray inline
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END && T.lf == ITEM_NONE) {

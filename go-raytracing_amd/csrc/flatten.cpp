@@ -880,6 +880,91 @@ struct Flattener {
     S.env_conditional.assign(cond.begin(), cond.end());
   }
 
+  // ---- BVH2 -> BVH4 collapse (device node form, DNode4).  Greedy top-down:
+  // a BVH4 node starts from a BVH2 node's two children and repeatedly opens
+  // the internal child with the largest surface area until it holds four
+  // children or only leaves remain.  Child boxes are the BVH2 boxes (already
+  // rounded outward), so every box test stays conservative and the hit
+  // results do not depend on the topology (DESIGN.md §Tie rule).
+  // `need` = stack entries the traversal may hold along the worst path
+  // below this item (a node with k hit children pushes k-1).
+  std::vector<int32_t> map4;   // BVH2 node -> BVH4 node (memo: shared BLASes)
+  std::vector<int32_t> need4;  // per BVH4 node
+  static double half_area(const float* b) {
+    const double dx = double(b[1]) - b[0], dy = double(b[3]) - b[2], dz = double(b[5]) - b[4];
+    if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+    if (std::isinf(dx) || std::isinf(dy) || std::isinf(dz)) return 1e300;
+    return dx * dy + dy * dz + dz * dx;
+  }
+  uint32_t collapse4(uint32_t item, int& need) {
+    need = 0;
+    if ((item >> ITEM_SHIFT) != ITEM_NODE) return item;
+    const uint32_t n2 = item & ITEM_MASK;
+    if (map4[n2] >= 0) { need = need4[map4[n2]]; return (ITEM_NODE << ITEM_SHIFT) | uint32_t(map4[n2]); }
+    struct Ch { uint32_t item; float box[6]; };
+    Ch ch[4];
+    int nc = 2;
+    {
+      const DNode& nd = S.nodes[n2];
+      ch[0].item = nd.litem; std::copy(nd.l, nd.l + 6, ch[0].box);
+      ch[1].item = nd.ritem; std::copy(nd.r, nd.r + 6, ch[1].box);
+    }
+    while (nc < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (int c = 0; c < nc; ++c)
+        if ((ch[c].item >> ITEM_SHIFT) == ITEM_NODE) {
+          const double a = half_area(ch[c].box);
+          if (a > ba) { ba = a; best = c; }
+        }
+      if (best < 0) break;
+      const DNode& nd = S.nodes[ch[best].item & ITEM_MASK];
+      Ch l, r;
+      l.item = nd.litem; std::copy(nd.l, nd.l + 6, l.box);
+      r.item = nd.ritem; std::copy(nd.r, nd.r + 6, r.box);
+      for (int c = nc; c > best + 1; --c) ch[c] = ch[c - 1];   // keep left-to-right order
+      ch[best] = l;
+      ch[best + 1] = r;
+      ++nc;
+    }
+    const int idx = int(S.nodes4.size());
+    S.nodes4.push_back(DNode4{});
+    map4[n2] = idx;
+    need4.push_back(0);
+    uint32_t items[4];
+    int worst = 0;
+    for (int c = 0; c < nc; ++c) {
+      int nn = 0;
+      items[c] = collapse4(ch[c].item, nn);
+      worst = std::max(worst, nn);
+    }
+    DNode4& o = S.nodes4[idx];
+    const float inf = std::numeric_limits<float>::infinity();
+    for (int c = 0; c < 4; ++c) {
+      const bool used = c < nc;
+      o.xlo[c] = used ? ch[c].box[0] : inf;  o.xhi[c] = used ? ch[c].box[1] : -inf;
+      o.ylo[c] = used ? ch[c].box[2] : inf;  o.yhi[c] = used ? ch[c].box[3] : -inf;
+      o.zlo[c] = used ? ch[c].box[4] : inf;  o.zhi[c] = used ? ch[c].box[5] : -inf;
+      o.item[c] = used ? items[c] : empty_leaf;
+    }
+    need = (nc - 1) + worst;
+    need4[idx] = need;
+    return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
+  }
+  void build_bvh4() {
+    map4.assign(S.nodes.size(), -1);
+    S.nodes4.clear();
+    need4.clear();
+    int n = 0;
+    S.tlas.root_item = collapse4(S.tlas.root_item, n);
+    S.tlas_need4 = n;
+    S.blas_need4 = 0;
+    for (DBvh& b : S.blas) {
+      b.root_item = collapse4(b.root_item, n);
+      S.blas_need4 = std::max(S.blas_need4, n);
+    }
+  }
+
   int run() {
     if (!d || !d->hittables || d->num_hittables <= 0) { fail(RT_ERR_INVALID, "empty scene"); return status; }
     if (!valid_index(d->root)) { fail(RT_ERR_INVALID, "bad root"); return status; }
@@ -917,11 +1002,13 @@ struct Flattener {
     lights();
     if (status) return status;
     environment();
-    // stack: one pending far child per world level + pending instances in a
-    // leaf + the INST_END marker + one per BLAS level.
-    S.stack_needed = S.tlas_depth + max_leaf_inst + 1 + S.blas_depth + 2;
+    build_bvh4();
+    // stack: pending siblings along the worst world path + pending instances
+    // in a leaf + the pending item and INST_END marker of an instance entry +
+    // pending siblings along the worst BLAS path.
+    S.stack_needed = S.tlas_need4 + max_leaf_inst + 1 + S.blas_need4 + 2;
     if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
-    if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27))
+    if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27) || S.nodes4.size() >= (1u << 27))
       fail(RT_ERR_UNSUPPORTED, "scene too large for 28-bit indices");
     return status;
   }

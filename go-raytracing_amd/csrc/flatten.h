@@ -8,7 +8,8 @@
 namespace rtg {
 
 struct HostScene {
-  std::vector<DNode> nodes;
+  std::vector<DNode> nodes;          // BVH2 (build form; probes)
+  std::vector<DNode4> nodes4;        // BVH4 collapsed from `nodes` (device form)
   std::vector<DLeaf> leaves;
   std::vector<uint32_t> refs;
   std::vector<int32_t> ref_rank;      // per ref (TLAS refs: DFS rank; others 0)
@@ -39,7 +40,8 @@ struct HostScene {
   float env_rotation = 0.f, env_total_power = 0.f;
   std::vector<float> env_texels, env_pdf, env_marginal, env_conditional;
   int stack_needed = 0;
-  int tlas_depth = 0, blas_depth = 0;
+  int tlas_depth = 0, blas_depth = 0;   // BVH2 levels
+  int tlas_need4 = 0, blas_need4 = 0;   // BVH4 stack entries along the worst root-to-leaf path
 };
 
 // How mesh BLASes are laid out (rt_ctx_set_option RT_OPT_BLAS_BUILDER).

@@ -25,9 +25,12 @@
 #include "device_common.h"
 #include "wavefront.h"
 
-// Minimum waves per SIMD requested for the traversal kernels (register cap).
+// Minimum waves per SIMD requested for the traversal kernels (register cap:
+// 5 waves = 96 VGPRs).  The traversal is latency- and issue-bound; measured
+// on CornellBoxLucy (BVH4): 4 waves 604, 5 waves 667, 6 waves 661 (spills),
+// 8 waves 620 Msamples/s.
 #ifndef RTG_TRAV_WAVES
-#define RTG_TRAV_WAVES 1
+#define RTG_TRAV_WAVES 5
 #endif
 
 namespace rtg {

@@ -24,7 +24,7 @@ static std::string first_fail;
 
 static void check_item(const HostScene& S, uint32_t it, const char* where) {
   const uint32_t tag = it >> ITEM_SHIFT, idx = it & ITEM_MASK;
-  if (tag == ITEM_NODE) CHECK(idx < S.nodes.size(), std::string(where) + ": node item out of range");
+  if (tag == ITEM_NODE) CHECK(idx < S.nodes4.size(), std::string(where) + ": node item out of range");
   else if (tag == ITEM_LEAF) CHECK(idx < S.leaves.size(), std::string(where) + ": leaf item out of range");
   else CHECK(false, std::string(where) + ": bad item tag");
 }
@@ -55,12 +55,46 @@ int main(int argc, char** argv) {
   CHECK(S.refs.size() == S.ref_rank.size(), "ref_rank size");
   CHECK(S.refs.size() == S.ref_box.size(), "ref_box size");
   CHECK(S.refs.size() == S.ref_top.size(), "ref_top size");
-  for (size_t i = 0; i < S.nodes.size(); ++i) {
-    check_item(S, S.nodes[i].litem, "node.l");
-    check_item(S, S.nodes[i].ritem, "node.r");
-  }
+  for (size_t i = 0; i < S.nodes4.size(); ++i)
+    for (int c = 0; c < 4; ++c) check_item(S, S.nodes4[i].item[c], "node4.item");
   check_item(S, S.tlas.root_item, "tlas root");
   for (const DBvh& b : S.blas) check_item(S, b.root_item, "blas root");
+  // The BVH4 reaches every leaf item exactly as often as a walk of the BVH2
+  // it was collapsed from (non-empty child slots only), and every child box
+  // of a BVH4 node contains the boxes inside that child.
+  {
+    std::vector<int> seen(S.leaves.size(), 0);
+    std::vector<uint32_t> st;
+    auto walk = [&](uint32_t root) {
+      st.assign(1, root);
+      while (!st.empty()) {
+        const uint32_t it = st.back();
+        st.pop_back();
+        if ((it >> ITEM_SHIFT) == ITEM_LEAF) { seen[it & ITEM_MASK]++; continue; }
+        if ((it >> ITEM_SHIFT) != ITEM_NODE || (it & ITEM_MASK) >= S.nodes4.size()) continue;
+        const DNode4& n = S.nodes4[it & ITEM_MASK];
+        for (int c = 0; c < 4; ++c)
+          if (n.xlo[c] <= n.xhi[c]) {
+            st.push_back(n.item[c]);
+            if ((n.item[c] >> ITEM_SHIFT) == ITEM_NODE && (n.item[c] & ITEM_MASK) < S.nodes4.size()) {
+              const DNode4& m = S.nodes4[n.item[c] & ITEM_MASK];
+              for (int e = 0; e < 4; ++e)
+                if (m.xlo[e] <= m.xhi[e])
+                  CHECK(m.xlo[e] >= n.xlo[c] && m.xhi[e] <= n.xhi[c] && m.ylo[e] >= n.ylo[c] && m.yhi[e] <= n.yhi[c] &&
+                            m.zlo[e] >= n.zlo[c] && m.zhi[e] <= n.zhi[c],
+                        "node4 child box not contained in its parent slot");
+            }
+          }
+      }
+    };
+    walk(S.tlas.root_item);
+    for (const DBvh& b : S.blas) walk(b.root_item);
+    // every leaf child of a BVH2 node is reached through the BVH4
+    for (const DNode& n : S.nodes)
+      for (uint32_t it : {n.litem, n.ritem})
+        if ((it >> ITEM_SHIFT) == ITEM_LEAF && (it & ITEM_MASK) != 0u)
+          CHECK(seen[it & ITEM_MASK] > 0, "BVH2 leaf not reached through the BVH4");
+  }
   int culled = 0;
   for (size_t li = 0; li < S.leaves.size(); ++li) {
     const DLeaf& L = S.leaves[li];

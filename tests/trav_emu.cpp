@@ -37,7 +37,7 @@ int main(int argc, char** argv) {
   std::string ferr;
   if (flatten_scene(rts_scene_get_desc(scn), h, ferr)) { fprintf(stderr, "%s\n", ferr.c_str()); return 4; }
   DScene d{};
-  d.nodes = ptr(h.nodes); d.leaves = ptr(h.leaves); d.refs = ptr(h.refs); d.ref_rank = ptr(h.ref_rank);
+  d.nodes = ptr(h.nodes4); d.leaves = ptr(h.leaves); d.refs = ptr(h.refs); d.ref_rank = ptr(h.ref_rank);
   d.ref_box = ptr(h.ref_box); d.spheres = ptr(h.spheres); d.quads = ptr(h.quads); d.tris = ptr(h.tris);
   d.tri_aux = ptr(h.tri_aux); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
