@@ -94,22 +94,26 @@ __device__ __forceinline__ TRay make_tray(V3 o, V3 d) {
 }
 
 // AABB.Hit (aabb.go:59-116) on a {xmin,xmax,ymin,ymax,zmin,zmax} box.
-// Returns the clamped entry distance in tnear.
-__device__ __forceinline__ bool slab(float bmin, float bmax, float o, float inv, float& tmin, float& tmax) {
-  float t0 = (bmin - o) * inv;
-  float t1 = (bmax - o) * inv;
-  if (inv < 0.0f) { float s = t0; t0 = t1; t1 = s; }
-  if (t0 > tmin) tmin = t0;
-  if (t1 < tmax) tmax = t1;
-  return tmax > tmin;
-}
+// Returns the clamped entry distance in tnear.  Per axis the reference
+// computes t0 = (min - o)*inv, t1 = (max - o)*inv, swaps them when inv < 0,
+// then narrows [tmin, tmax] with "if t0 > tmin" / "if t1 < tmax" (a NaN from
+// 0*inf leaves the bound unchanged) and fails once tmax <= tmin.  Here:
+//   * the swap is a select of the plane before the subtraction (same
+//     operands, same operations, bit-identical t0/t1);
+//   * the narrowing is fmaxf/fminf, which also return the other operand for
+//     a NaN (v_max/v_min, max3/min3 chains);
+//   * one final tmax > tmin test, equivalent to the per-axis early exits
+//     because the bounds only narrow.
 __device__ __forceinline__ bool box_hit(float x0, float x1, float y0, float y1, float z0, float z1,
                                         const TRay& r, float tmin, float tmax, float& tnear) {
-  bool a = slab(x0, x1, r.o.x, r.inv.x, tmin, tmax);
-  bool b = slab(y0, y1, r.o.y, r.inv.y, tmin, tmax);
-  bool c = slab(z0, z1, r.o.z, r.inv.z, tmin, tmax);
+  const bool sx = r.inv.x < 0.0f, sy = r.inv.y < 0.0f, sz = r.inv.z < 0.0f;
+  const float tx0 = ((sx ? x1 : x0) - r.o.x) * r.inv.x, tx1 = ((sx ? x0 : x1) - r.o.x) * r.inv.x;
+  const float ty0 = ((sy ? y1 : y0) - r.o.y) * r.inv.y, ty1 = ((sy ? y0 : y1) - r.o.y) * r.inv.y;
+  const float tz0 = ((sz ? z1 : z0) - r.o.z) * r.inv.z, tz1 = ((sz ? z0 : z1) - r.o.z) * r.inv.z;
+  tmin = fmaxf(fmaxf(fmaxf(tmin, tx0), ty0), tz0);
+  tmax = fminf(fminf(fminf(tmax, tx1), ty1), tz1);
   tnear = tmin;
-  return a && b && c;   // monotone: equivalent to the early-exit form
+  return tmax > tmin;
 }
 
 // ----------------------------------------------------------------------------
