@@ -288,6 +288,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   a.spill_cap = kStackMax - stack;
   if ((rc = ensure(ctx, ctx->wspill, size_t(a.spill_lanes) * size_t(a.spill_cap) * sizeof(uint32_t)))) return rc;
   a.spill = static_cast<uint32_t*>(ctx->wspill.p);
+  a.slots = uint32_t(S);
   if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(hipEventRecord(ctx->kev0, st));
   HIPCHK(launch_wavefront(ctx->dscene, dc, a, plan, stack, count, d_out, p->accumulate ? 1 : 0, st));
@@ -513,6 +514,10 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed;
   d.has_volumes = h.volumes.empty() ? 0 : 1;
+  d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
+  d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
+  d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
+  d.n_volumes = uint32_t(h.volumes.size());
   d.has_fancy = 0;
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;

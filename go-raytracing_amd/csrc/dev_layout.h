@@ -213,6 +213,8 @@ struct DScene {
   int32_t stack_needed;
   int32_t has_volumes;
   int32_t has_fancy;      // a Metal / Dielectric / Isotropic material exists
+  // array lengths (bounds checks of the RTG_GUARD diagnostic build)
+  uint32_t n_nodes, n_leaves, n_refs, n_spheres, n_quads, n_tris, n_instances, n_blas, n_volumes;
 };
 
 struct DCamera {

@@ -8,6 +8,24 @@
 
 namespace rtg {
 
+// RTG_GUARD (diagnostic build only, never the product): every device array
+// index is checked against its length; a bad index is reported once per
+// site class by printf and clamped, so a bad index shows up as a message
+// instead of a memory fault.
+#ifdef RTG_GUARD
+__device__ int rtg_guard_hits;
+__device__ __forceinline__ uint32_t rtg_gix(uint32_t i, uint32_t n, int site) {
+  if (i >= n) {
+    if (atomicAdd(&rtg_guard_hits, 1) < 16) printf("RTG_GUARD site %d: index %u >= %u\n", site, i, n);
+    return n ? n - 1u : 0u;
+  }
+  return i;
+}
+#define GIX(i, n, site) rtg_gix(uint32_t(i), uint32_t(n), site)
+#else
+#define GIX(i, n, site) (i)
+#endif
+
 // ----------------------------------------------------------------------------
 // Vec3 (vec3.go) in fp32, same operation order as Go.
 // ----------------------------------------------------------------------------
@@ -263,7 +281,7 @@ __device__ __forceinline__ void to_object(const DInstance& in, V3& o, V3& d) {
 // (Surrounds: spheres, planes).  Keys make that order-independent.
 // ----------------------------------------------------------------------------
 struct Best {
-  float t;
+  float t = 0.0f;
   int kind;      // PK_*; 0 = none
   int idx;       // prim / volume / plane index
   int inst;      // instance id or -1
@@ -274,14 +292,16 @@ struct Best {
 __device__ __forceinline__ bool closed_kind(int k) { return k == PK_QUAD || k == PK_TRI || k == PK_VOLUME; }
 
 __device__ __forceinline__ int obj_rank(const DScene& sc, int refpos) {
-  return refpos >= 0 ? sc.ref_rank[refpos] : sc.planes[-1 - refpos].rank;
+  return refpos >= 0 ? sc.ref_rank[GIX(refpos, sc.n_refs, 27)] : sc.planes[GIX(-1 - refpos, sc.num_planes, 28)].rank;
 }
 // Rank of a primitive inside its BLAS in the reference's DFS order.  primpos
 // is the primitive array index, or (bit 31 set) the refs index for mixed
 // leaves.  Only read on exact t ties.
 __device__ __forceinline__ int prim_rank(const DScene& sc, int kind, int primpos) {
-  if (primpos < 0) return sc.ref_rank[primpos & 0x7FFFFFFF];
-  return kind == PK_TRI ? sc.tri_rank[primpos] : kind == PK_QUAD ? sc.quad_rank[primpos] : sc.sphere_rank[primpos];
+  const int pos = primpos & 0x3FFFFFFF;
+  if (primpos < 0) return sc.ref_rank[GIX(pos, sc.n_refs, 29)];
+  return kind == PK_TRI ? sc.tri_rank[GIX(pos, sc.n_tris, 30)]
+         : kind == PK_QUAD ? sc.quad_rank[GIX(pos, sc.n_quads, 31)] : sc.sphere_rank[GIX(pos, sc.n_spheres, 32)];
 }
 // Is candidate (kind, refpos, primpos) preferred over the best at equal t?
 // Rare (exact float ties), scalar arguments only.
@@ -314,15 +334,20 @@ struct Cnt {
 // over a list leaf.  ntests = how many times the enclosing leaf calls Hit
 // (2 for the BVHNode{leaf,leaf} wrapper): the reference then keeps the
 // smaller of the independent free-flight draws, i.e. U = max(U_1..U_n).
+#if defined(RTG_VOLUME_NOINLINE) && !defined(RTG_HOST_EMU)
+#define RTG_VOLUME_ATTR __attribute__((noinline))
+#else
+#define RTG_VOLUME_ATTR
+#endif
 template <bool kCount>
-__device__ bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, float time,
+__device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, float time,
                            float tmin, float tmax, int ntests, uint32_t key, uint32_t bounce,
                            uint32_t dom, float& t_out, Cnt& cnt) {
-  const DInstance& bi = sc.instances[vol.boundary];
+  const DInstance& bi = sc.instances[GIX(vol.boundary, sc.n_instances, 1)];
   V3 o = wo, d = wd;
   to_object(bi, o, d);
-  const DBvh& bb = sc.blas[bi.blas];
-  DLeaf lf = sc.leaves[bb.root_item & ITEM_MASK];
+  const DBvh& bb = sc.blas[GIX(bi.blas, sc.n_blas, 2)];
+  DLeaf lf = sc.leaves[GIX(bb.root_item & ITEM_MASK, sc.n_leaves, 3)];
   int n = leaf_count(lf.info), kind = leaf_kind(lf.info);
   // rec1: closest over the universe interval; rec2: closest over (t1+1e-4, inf).
   float t1 = __builtin_inff(), t2 = __builtin_inff();
@@ -333,12 +358,12 @@ __device__ bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, f
     bool found = false;
     for (int k = 0; k < n; ++k) {
       int pk = kind; uint32_t pi = lf.first + k;
-      if (kind == PK_MIXED) { uint32_t r = sc.refs[pi]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
-      float t;
+      if (kind == PK_MIXED) { uint32_t r = sc.refs[GIX(pi, sc.n_refs, 4)]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
+      float t = 0.0f;
       bool ok = false;
-      if (pk == PK_QUAD) { ok = quad_t(sc.quads[pi], o, d, lo, t) && t <= closest; }
-      else if (pk == PK_TRI) { ok = tri_t(sc.tris[pi], o, d, lo, t) && t <= closest; }
-      else if (pk == PK_SPHERE) { ok = sphere_t(sc.spheres[pi], o, d, time, lo, t) && t < closest; }
+      if (pk == PK_QUAD) { ok = quad_t(sc.quads[GIX(pi, sc.n_quads, 5)], o, d, lo, t) && t <= closest; }
+      else if (pk == PK_TRI) { ok = tri_t(sc.tris[GIX(pi, sc.n_tris, 6)], o, d, lo, t) && t <= closest; }
+      else if (pk == PK_SPHERE) { ok = sphere_t(sc.spheres[GIX(pi, sc.n_spheres, 7)], o, d, time, lo, t) && t < closest; }
       if (ok) { closest = t; found = true; }
     }
     if (pass == 0) { h1 = found; t1 = closest; if (!h1) break; }
@@ -382,6 +407,9 @@ constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the sta
 // the reused slot to this lane's spill area in global memory (`spill_cap`
 // more entries, rarely touched); popping below that depth brings it back.
 // Deep BVHs therefore cost LDS only for the top of the stack.
+// The lane's world-space ray (origin, direction, 1/direction) lives beside it
+// in LDS: it is read only on instance entry / exit and volume tests, so it
+// need not occupy nine VGPRs for the whole traversal.
 struct TStack {
   uint32_t* lds;       // this lane's slot 0
   int stride;          // LDS words between slots (lanes interleaved)
@@ -389,45 +417,72 @@ struct TStack {
   uint32_t* spill;     // this lane's spill entry 0 (nullptr: spill_cap == 0)
   int sstride;         // words between spill entries
   int spill_cap;
+  float* wr;           // this lane's world ray: 9 floats, `stride` apart
+#ifdef RTG_WORLD_RAY_REGS
+  mutable V3 wo_, wd_, winv_;
+  __device__ __forceinline__ void save_world(V3 o, V3 d, V3 inv) const { wo_ = o; wd_ = d; winv_ = inv; }
+  __device__ __forceinline__ V3 wo() const { return wo_; }
+  __device__ __forceinline__ V3 wd() const { return wd_; }
+  __device__ __forceinline__ V3 winv() const { return winv_; }
+#else
+  __device__ __forceinline__ void save_world(V3 o, V3 d, V3 inv) const {
+    wr[0] = o.x; wr[stride] = o.y; wr[2 * stride] = o.z;
+    wr[3 * stride] = d.x; wr[4 * stride] = d.y; wr[5 * stride] = d.z;
+    wr[6 * stride] = inv.x; wr[7 * stride] = inv.y; wr[8 * stride] = inv.z;
+  }
+  __device__ __forceinline__ V3 wo() const { return mk(wr[0], wr[stride], wr[2 * stride]); }
+  __device__ __forceinline__ V3 wd() const { return mk(wr[3 * stride], wr[4 * stride], wr[5 * stride]); }
+  __device__ __forceinline__ V3 winv() const { return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]); }
+#endif
   __device__ __forceinline__ void push(int sp, uint32_t v) const {
     uint32_t* slot = lds + (sp & (cap - 1)) * stride;
-    if (sp >= cap) spill[(sp - cap) * sstride] = *slot;
+    if (sp >= cap) spill[size_t(GIX(sp - cap, spill_cap, 25)) * sstride] = *slot;
     *slot = v;
   }
   __device__ __forceinline__ uint32_t pop(int sp) const {   // sp = new depth
     uint32_t* slot = lds + (sp & (cap - 1)) * stride;
     const uint32_t v = *slot;
-    if (sp >= cap) *slot = spill[(sp - cap) * sstride];
+    if (sp >= cap) *slot = spill[size_t(GIX(sp - cap, spill_cap, 26)) * sstride];
     return v;
   }
 };
+// LDS words per lane: `cap` stack entries + the 9-float world ray.
 __device__ __forceinline__ TStack lds_stack_only(uint32_t* lds, int stride, int cap) {
-  return TStack{lds, stride, cap, nullptr, 0, 0};
+  return TStack{lds, stride, cap, nullptr, 0, 0, reinterpret_cast<float*>(lds + cap * stride)};
 }
 
 // Resumable traversal state (one lane, one ray).
+// The world-space ray is kept in the TStack's LDS area (TStack::wr).
 struct Trav {
-  V3 wo, wd, winv;       // world-space ray (instances / volumes / restore)
   TRay cr;               // current-space ray (object space inside an instance)
   float time, tmin, tmax;
   uint32_t key, bounce, voldom;
   uint32_t item, lf;
-  int sp, cur_inst, cur_ref;
-  Best best;
+  int sp, cur_ref;       // cur_ref: TLAS ref of the instance being traversed, -1 in world space
+  Best best;             // best.inst is resolved once at the end (resolve_inst)
 };
+
+// Best.primpos flags: bit 31 = mixed-leaf ref position, bit 30 = the hit lies
+// inside an instance (its instance is refs[refpos]); low 30 bits = position.
+constexpr int PRIM_MIXED = int(0x80000000u);
+constexpr int PRIM_IN_INST = 0x40000000;
+__device__ __forceinline__ void resolve_inst(const DScene& sc, Best& b) {
+  b.inst = (b.kind != 0 && (b.primpos & PRIM_IN_INST)) ? int(sc.refs[GIX(b.refpos, sc.n_refs, 8)] & REF_MASK) : -1;
+}
 
 enum : int { TRAV_RUNNING = 0, TRAV_DONE = 1, TRAV_ANYHIT = 2 };
 
 // Set up one ray: planes (lifted out of the BVH) and the root box.
 template <bool kAny, bool kCount>
-__device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, V3 wo, V3 wd, float time, float tmin, float tmax,
-                                         uint32_t key, uint32_t bounce, uint32_t voldom, Cnt& cnt) {
-  T.wo = wo; T.wd = wd; T.time = time; T.tmin = tmin; T.tmax = tmax;
+__device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack& S, V3 wo, V3 wd, float time,
+                                         float tmin, float tmax, uint32_t key, uint32_t bounce, uint32_t voldom,
+                                         Cnt& cnt) {
+  T.time = time; T.tmin = tmin; T.tmax = tmax;
   T.key = key; T.bounce = bounce; T.voldom = voldom;
   Best& best = T.best;
   best.t = tmax; best.kind = 0; best.idx = -1; best.inst = -1; best.refpos = 0; best.primpos = 0;
   for (int i = 0; i < sc.num_planes; ++i) {
-    float t;
+    float t = 0.0f;
     if (kCount) cnt.plane++;
     if (plane_t(sc.planes[i], wo, wd, tmin, t)) {
       if (kAny) { if (t < tmax) return TRAV_ANYHIT; }
@@ -437,10 +492,10 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, V3 wo, V3 wd
     }
   }
   T.cr = make_tray(wo, wd);
-  T.winv = T.cr.inv;
-  T.cur_inst = -1; T.cur_ref = -1; T.sp = 0;
+  S.save_world(wo, wd, T.cr.inv);
+  T.cur_ref = -1; T.sp = 0;
   T.item = ITEM_NONE; T.lf = ITEM_NONE;
-  float tn;
+  float tn = 0.0f;
   if (sc.tlas.check_box &&
       !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
                T.cr, tmin, kAny ? tmax : best.t, tn))
@@ -473,7 +528,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
-    const float4* np = reinterpret_cast<const float4*>(sc.nodes + (T.item & ITEM_MASK));
+    const float4* np = reinterpret_cast<const float4*>(sc.nodes + GIX(T.item & ITEM_MASK, sc.n_nodes, 9));
     const float4 xl = np[0], xh = np[1], yl = np[2], yh = np[3], zl = np[4], zh = np[5];
     const uint4 it = reinterpret_cast<const uint4*>(np)[6];
     if (kCount) cnt.nodes++;
@@ -505,7 +560,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     }
     // leaving an instance with nothing postponed: restore the world ray inline
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END && T.lf == ITEM_NONE) {
-      T.cr.o = T.wo; T.cr.d = T.wd; T.cr.inv = T.winv; T.cur_inst = -1; T.cur_ref = -1;
+      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
@@ -515,70 +570,70 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   while (T.lf != ITEM_NONE) {
     const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
     if (tag == ITEM_LEAF) {
-      const DLeaf leaf = sc.leaves[idx];
+      const DLeaf leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
       const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
-      const bool world = T.cur_inst < 0;
+      const bool world = T.cur_ref < 0;
       for (int k = 0; k < n; ++k) {
         int pk = kind;
         uint32_t pi = leaf.first + k;
         const int pos = int(leaf.first) + k;
-        if (kind == PK_MIXED) { const uint32_t r = sc.refs[pi]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
-        float t;
+        if (kind == PK_MIXED) { const uint32_t r = sc.refs[GIX(pi, sc.n_refs, 11)]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
+        float t = 0.0f;
         bool ok = false;
         if (pk == PK_TRI) {
           if (kCount) cnt.tri++;
-          ok = tri_t(sc.tris[pi], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
+          ok = tri_t(sc.tris[GIX(pi, sc.n_tris, 12)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
         } else if (pk == PK_QUAD) {
           if (kCount) cnt.quad++;
-          ok = quad_t(sc.quads[pi], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
+          ok = quad_t(sc.quads[GIX(pi, sc.n_quads, 13)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
         } else if (pk == PK_SPHERE) {
           if (kCount) cnt.sph++;
-          ok = sphere_t(sc.spheres[pi], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+          ok = sphere_t(sc.spheres[GIX(pi, sc.n_spheres, 14)], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
         } else if (pk == PK_INSTANCE) {
           // world-space cull on the instance's own (padded) bbox before
           // paying for the instance fetch + object-space root test
-          const float4* bp = reinterpret_cast<const float4*>(sc.ref_box + pos);
+          const float4* bp = reinterpret_cast<const float4*>(sc.ref_box + GIX(pos, sc.n_refs, 15));
           const float4 lo = bp[0], hi = bp[1];
-          float tn;
+          float tn = 0.0f;
           if (kCount) cnt.ibox++;
           if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : best.t, tn)) continue;
           if (!push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos))) return TRAV_DONE;
           continue;
         } else if (kVol && pk == PK_VOLUME) {
-          ok = volume_hit<kCount>(sc, sc.volumes[pi], T.wo, T.wd, T.time, T.tmin, kAny ? T.tmax : best.t,
+          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), T.time, T.tmin, kAny ? T.tmax : best.t,
                                   leaf_ntests(leaf.info), T.key, T.bounce, T.voldom, t, cnt);
         }
         if (!ok) continue;
         if (kAny) return TRAV_ANYHIT;
         const int refpos = world ? pos : T.cur_ref;
-        const int primpos = world ? 0 : (kind == PK_MIXED ? int(uint32_t(pos) | 0x80000000u) : pos);
+        const int primpos = world ? 0 : ((kind == PK_MIXED ? PRIM_MIXED : 0) | PRIM_IN_INST | pos);
         if (accept(sc, t, pk, refpos, primpos, best)) {
-          best.t = t; best.kind = pk; best.idx = int(pi); best.inst = T.cur_inst;
+          best.t = t; best.kind = pk; best.idx = int(pi);
           best.refpos = refpos; best.primpos = primpos;
         }
       }
     } else if (tag == ITEM_INSTANCE) {
-      const uint32_t r = sc.refs[idx];
+      const uint32_t r = sc.refs[GIX(idx, sc.n_refs, 17)];
       const int ii = int(r & REF_MASK);
-      const DInstance& in = sc.instances[ii];
+      const DInstance& in = sc.instances[GIX(ii, sc.n_instances, 18)];
       if (kCount) cnt.inst++;
-      V3 o = T.wo, d = T.wd;
+      V3 o = S.wo(), d = S.wd();
       to_object(in, o, d);
       const TRay orr = make_tray(o, d);
-      const DBvh& bb = sc.blas[in.blas];
+      const DBvh& bb = sc.blas[GIX(in.blas, sc.n_blas, 19)];
       bool enter = true;
-      float tn;
+      float tn = 0.0f;
       if (bb.check_box)
         enter = box_hit(bb.box[0], bb.box[1], bb.box[2], bb.box[3], bb.box[4], bb.box[5], orr, T.tmin,
                         kAny ? T.tmax : best.t, tn);
       if (enter) {
         if (T.item < ITEM_POP && !push(T.item)) return TRAV_DONE;
         if (!push(ITEM_INST_END << ITEM_SHIFT)) return TRAV_DONE;
-        T.cr = orr; T.cur_inst = ii; T.cur_ref = int(idx);
+        T.cr = orr; T.cur_ref = int(idx);
         T.item = bb.root_item;
       }
     } else {  // ITEM_INST_END: back to the world-space ray
-      T.cr.o = T.wo; T.cr.d = T.wd; T.cr.inv = T.winv; T.cur_inst = -1; T.cur_ref = -1;
+      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
     }
     T.lf = ITEM_NONE;
     // ITEM_NONE here only means the stack was empty when this lane last
@@ -594,10 +649,11 @@ template <bool kAny, bool kCount, bool kVol = true>
 __device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin, float tmax,
                          const TStack& S, Best& best, uint32_t key,
                          uint32_t bounce, uint32_t voldom, Cnt& cnt, int* err) {
-  Trav T;
-  int s = trav_init<kAny, kCount>(sc, T, wo, wd, time, tmin, tmax, key, bounce, voldom, cnt);
+  Trav T{};   // fully initialised: no undef state flows through the divergent loop
+  int s = trav_init<kAny, kCount>(sc, T, S, wo, wd, time, tmin, tmax, key, bounce, voldom, cnt);
   while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol>(sc, T, S, cnt, err);
   best = T.best;
+  if (!kAny) resolve_inst(sc, best);
   if (kAny) return s == TRAV_ANYHIT;
   return best.kind != 0;
 }
@@ -626,7 +682,7 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
     return rec;
   }
   if (b.kind == PK_VOLUME) {                       // volume.go:72-76
-    const DVolume& v = sc.volumes[b.idx];
+    const DVolume& v = sc.volumes[GIX(b.idx, sc.n_volumes, 20)];
     rec.P = add(wo, scale(wd, b.t));
     rec.N = mk(1.0f, 0.0f, 0.0f);
     rec.front = true;
@@ -635,19 +691,19 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
   }
   V3 o = wo, d = wd;
   const DInstance* in = nullptr;
-  if (b.inst >= 0) { in = &sc.instances[b.inst]; to_object(*in, o, d); }
+  if (b.inst >= 0) { in = &sc.instances[GIX(b.inst, sc.n_instances, 21)]; to_object(*in, o, d); }
   rec.P = add(o, scale(d, b.t));
   if (b.kind == PK_SPHERE) {
-    const DSphere& s = sc.spheres[b.idx];
+    const DSphere& s = sc.spheres[GIX(b.idx, sc.n_spheres, 22)];
     V3 c = add(mk(s.cx, s.cy, s.cz), scale(mk(s.vx, s.vy, s.vz), time));
     set_face(d, divs(sub(rec.P, c), s.r), rec);
     rec.mat = s.mat;
   } else if (b.kind == PK_QUAD) {
-    const DQuad& q = sc.quads[b.idx];
+    const DQuad& q = sc.quads[GIX(b.idx, sc.n_quads, 23)];
     set_face(d, mk(q.nx, q.ny, q.nz), rec);
     rec.mat = q.mat;
   } else {  // PK_TRI
-    const DTriAux& ax = sc.tri_aux[b.idx];
+    const DTriAux& ax = sc.tri_aux[GIX(b.idx, sc.n_tris, 24)];
     set_face(d, mk(ax.nx, ax.ny, ax.nz), rec);
     rec.mat = ax.mat;
   }
@@ -765,7 +821,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
   bool allow = true;
   uint32_t bounce = 0;
   for (int dleft = depth; dleft > 0; --dleft, ++bounce) {
-    Best b;
+    Best b{};
     if (kCount) cnt.rays++;
     bool hit = traverse<false, kCount>(sc, ro, rd, time, 0.001f, __builtin_inff(), S, b, key,
                                        bounce, DOM_VOL, cnt, err);
@@ -854,7 +910,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
         }
         float cth = dot(rec.N, ldir);
         if (cth > 0.0f) {
-          Best sb;
+          Best sb{};
           if (kCount) cnt.shadow++;
           bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, __builtin_inff(), S,
                                                 sb, key, bounce, DOM_VOL_SH_HDRI, cnt, err);
@@ -877,7 +933,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
           V3 ldir = unit(tl);
           float cth = dot(rec.N, ldir);
           if (cth > 0.0f) {
-            Best sb;
+            Best sb{};
             if (kCount) cnt.shadow++;
             bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, dist - 0.001f, S,
                                                   sb, key, bounce, DOM_VOL_SH_AREA, cnt, err);

@@ -38,7 +38,7 @@ namespace rtg {
 // ----------------------------------------------------------------------------
 template <int STACK, bool kCount>
 __global__ __launch_bounds__(256) void render_kernel(DScene sc, DCamera cam, RenderLaunch w) {
-  __shared__ uint32_t lds_stack[STACK * 256];
+  __shared__ uint32_t lds_stack[(STACK + 9) * 256];   // stack + world ray
   const int tid = threadIdx.x;
   const int tile = blockIdx.x / w.chunks;
   const int chunk = blockIdx.x - tile * w.chunks;
@@ -120,7 +120,7 @@ __global__ void tonemap_kernel(const float* accum, int n, int spp, uint8_t* rgba
 template <int STACK>
 __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, uint32_t seed, int sample,
                                                       int32_t* out_top, int32_t* out_prim, float* out_t, int* err) {
-  __shared__ uint32_t lds_stack[STACK * 256];
+  __shared__ uint32_t lds_stack[(STACK + 9) * 256];   // stack + world ray
   const int tid = threadIdx.x;
   const int i = blockIdx.x * 256 + tid;
   if (i >= cam.width * cam.height) return;
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, ui
     ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
   }
   V3 rd = sub(ps, ro);
-  Best b;
+  Best b{};
   Cnt cnt = {};
   bool hit = traverse<false, false>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack_only(lds_stack + tid, 256, STACK), b, key,
                                     0, DOM_VOL, cnt, err);

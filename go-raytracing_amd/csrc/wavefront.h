@@ -41,6 +41,7 @@ struct WaveArgs {
   uint32_t* spill;  // traversal-stack spill area: spill_cap entries x spill_lanes
   uint32_t spill_lanes;
   int32_t spill_cap;
+  uint32_t slots;   // capacity of every per-slot array (RTG_GUARD bounds checks)
 };
 
 // L target of a NEE record: the survivor's next-stream position, or the

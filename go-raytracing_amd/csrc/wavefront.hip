@@ -26,12 +26,23 @@
 #include "wavefront.h"
 
 // Minimum waves per SIMD requested for the traversal kernels (register cap:
-// 5 waves = 96 VGPRs).  The traversal is latency- and issue-bound; measured
-// on CornellBoxLucy (BVH4): 4 waves 604, 5 waves 667, 6 waves 661 (spills),
-// 8 waves 620 Msamples/s.
+// 6 waves = 80 VGPRs; the LDS ring + world ray, 25.6 KB per block, also
+// allows 6).  The traversal is latency- and issue-bound; measured on
+// CornellBoxLucy with the world ray in LDS: 5 waves 681, 6 waves 745
+// Msamples/s (1-3 VGPRs spilled).
 #ifndef RTG_TRAV_WAVES
-#define RTG_TRAV_WAVES 5
+#define RTG_TRAV_WAVES 6
 #endif
+// The volume (fog) and instrumented variants carry more live state: at the
+// 96-VGPR cap they spill 40-120 VGPRs to scratch, so they keep 4 waves
+// (128 VGPRs) and compile without VGPR spills.
+// LDS words per lane beside the stack ring: the world ray (TStack::wr)
+#ifdef RTG_WORLD_RAY_REGS
+#define RTG_WR_WORDS 0
+#else
+#define RTG_WR_WORDS 9
+#endif
+#define RTG_TRAV_WAVES_FOR(kVol, kCount) (((kVol) || (kCount)) ? 4 : RTG_TRAV_WAVES)
 
 namespace rtg {
 
@@ -132,7 +143,8 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   return idx;
 }
 
-__device__ __forceinline__ void store_hit(float4* hit, uint32_t p, const Best& b) {
+__device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
+  resolve_inst(sc, b);
   hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
                        0.0f);
 }
@@ -142,18 +154,19 @@ __device__ __forceinline__ void store_hit(float4* hit, uint32_t p, const Best& b
 // the prefetch's loads are in flight while the lane traverses, so a lane
 // that finishes starts its next ray on the following step without waiting.
 template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_extend(DScene sc, WaveArgs a, PathStream cs,
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_extend(DScene sc, WaveArgs a, PathStream cs,
                                                                 const uint32_t* count, uint32_t* zero_a,
                                                                 uint32_t* zero_b, uint32_t* zero_c, uint32_t* fetch) {
-  __shared__ uint32_t lds_stack[STACK * 256];
+  __shared__ uint32_t lds_stack[(STACK + RTG_WR_WORDS) * 256];   // stack ring + world ray
   // next stream's count, the shadow job count and the shadow fetch counter
   if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
   const uint32_t n = *count;
-  const uint32_t nwaves = gridDim.x * (blockDim.x / 64u);
+  const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap};
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap,
+                 reinterpret_cast<float*>(lds_stack + STACK * 256 + threadIdx.x)};
   Cnt cnt = {};
-  Trav T;
+  Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool P{0u, 0u, false};
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   float4 po = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pd = po;
@@ -163,16 +176,16 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_extend(DScene sc, WaveA
       p = pn;
       pn = ITEM_NONE;
       if (kCount) cnt.rays++;
-      const int s = trav_init<false, kCount>(sc, T, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), po.w, 0.001f,
+      const int s = trav_init<false, kCount>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), po.w, 0.001f,
                                              __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
-      if (s != TRAV_RUNNING) { store_hit(a.hit, p, T.best); p = ITEM_NONE; }
+      if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
-      pn = idx;
-      po = cs.o[idx];
-      pd = cs.d[idx];
-      if (kVol) pb = (asu(cs.beta[idx].w) >> 16) & 0x7FFFu;
+      pn = GIX(idx, a.slots, 40);
+      po = cs.o[pn];
+      pd = cs.d[pn];
+      if (kVol) pb = (asu(cs.beta[pn].w) >> 16) & 0x7FFFu;
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (P.dry) break;
@@ -180,7 +193,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_extend(DScene sc, WaveA
     }
     if (p != ITEM_NONE) {
       const int s = trav_step<false, kCount, kVol>(sc, T, S, cnt, a.err);
-      if (s != TRAV_RUNNING) { store_hit(a.hit, p, T.best); p = ITEM_NONE; }
+      if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
     }
   }
   if (kCount) add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
@@ -196,11 +209,13 @@ __device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, u
   const int w = int(threadIdx.x >> 6);
   if (__lane_id() == 0) { sw[0][w] = uint32_t(__popcll(m0)); sw[1][w] = uint32_t(__popcll(m1)); }
   __syncthreads();
-  if (threadIdx.x < 2u) {
-    const int q = int(threadIdx.x);
-    uint32_t tot = 0;
-    for (int k = 0; k < 4; ++k) { const uint32_t c = sw[q][k]; sw[q][k] = tot; tot += c; }
-    sb[q] = tot ? atomicAdd(q ? q1 : q0, tot) : 0u;
+  if (threadIdx.x == 0u) {
+    const int nw = int((blockDim.x + 63u) >> 6);
+    for (int q = 0; q < 2; ++q) {
+      uint32_t tot = 0;
+      for (int k = 0; k < nw; ++k) { const uint32_t c = sw[q][k]; sw[q][k] = tot; tot += c; }
+      sb[q] = tot ? atomicAdd(q ? q1 : q0, tot) : 0u;
+    }
   }
   __syncthreads();
   p0 = sb[0] + sw[0][w] + lanes_below(m0);
@@ -246,7 +261,8 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
     float time = 0.0f, tmax_a = 0.0f;
     V3 L = mk(0.0f, 0.0f, 0.0f), P = L, sd = L, beta = L, nbeta = L, ca = L, ch = L, da = L, dh = L;
     if (live) {
-      const float4 h = a.hit[i], o4 = cs.o[i], d4 = cs.d[i], b4 = cs.beta[i], L4 = cs.L[i];
+      const uint32_t ii = GIX(i, a.slots, 41);
+      const float4 h = a.hit[ii], o4 = cs.o[ii], d4 = cs.d[ii], b4 = cs.beta[ii], L4 = cs.L[ii];
       key = asu(d4.w);
       slot = asu(L4.w);
       const uint32_t st = asu(b4.w);
@@ -258,6 +274,10 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
       beta = mk(b4.x, b4.y, b4.z);
       L = mk(L4.x, L4.y, L4.z);
       const uint32_t kh = asu(h.y);
+#ifdef RTG_GUARD
+      if (kh == 0xFFFFFFFFu && atomicAdd(&rtg_guard_hits, 1) < 16)
+        printf("RTG_GUARD site 50: hit %u of %u never written (bounce %u)\n", i, n, (asu(b4.w) >> 16) & 0x7FFFu);
+#endif
       if (kh == 0u) {                                            // miss (camera.go:451-466)
         V3 bg;
         if (sc.env.valid) {
@@ -272,12 +292,12 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
         }
         L = add(L, mul(beta, bg));
       } else {
-        Best b;
+        Best b{};
         b.t = h.x; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = int(asu(h.z));
         b.refpos = 0; b.primpos = 0;
         Rec rec = make_record(sc, b, ro, rd, time);
         P = rec.P;
-        const DMaterial& m = sc.materials[rec.mat];
+        const DMaterial& m = sc.materials[GIX(rec.mat, sc.num_materials, 42)];
         if (kCount) cnt.mat++;
         V3 att = mk(0.0f, 0.0f, 0.0f);
         bool scat = true, use_mis = false;
@@ -394,17 +414,20 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
         }
       }
     }
-    uint32_t jc, js;
+    uint32_t jc = 0, js = 0;
     block_reserve2(cont, want_shadow, ncount, a.counts + CNT_SHADOW, s_w[par], s_b[par], jc, js);
     if (cont) {
+      jc = GIX(jc, a.slots, 43);
       ns.o[jc] = make_float4(P.x, P.y, P.z, time);
       ns.d[jc] = make_float4(sd.x, sd.y, sd.z, asf(key));
       ns.beta[jc] = make_float4(nbeta.x, nbeta.y, nbeta.z, asf(nstate));
       ns.L[jc] = make_float4(L.x, L.y, L.z, asf(slot));
     } else if (live) {
+      slot = GIX(slot, a.slots, 44);
       a.Lout[slot] = make_float4(L.x, L.y, L.z, 0.0f);
     }
     if (want_shadow) {
+      js = GIX(js, a.slots, 45);
       a.sj_p[js] = make_float4(P.x, P.y, P.z, asf(key));
       a.sj_a[js] = make_float4(da.x, da.y, da.z, tmax_a);
       if (kEnvIS) a.sj_h[js] = make_float4(dh.x, dh.y, dh.z, 0.0f);
@@ -423,16 +446,17 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
 // contributions in that order, camera.go:549-558).  Lanes prefetch their next
 // job as k_extend does.
 template <int STACK, bool kCount, bool kVol, bool kEnvIS>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
-  __shared__ uint32_t lds_stack[STACK * 256];
+  __shared__ uint32_t lds_stack[(STACK + RTG_WR_WORDS) * 256];   // stack ring + world ray
   if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
   const uint32_t n = *count;
-  const uint32_t nwaves = gridDim.x * (blockDim.x / 64u);
+  const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap};
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap,
+                 reinterpret_cast<float*>(lds_stack + STACK * 256 + threadIdx.x)};
   Cnt cnt = {};
-  Trav T;
+  Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool Q{0u, 0u, false};
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   // current job
@@ -445,7 +469,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_shadow(DScene sc, WaveA
   uint32_t qinfo = 1u;
   auto start_ray = [&](int rr, V3 dir, float tmax) -> int {
     if (kCount) cnt.shadow++;
-    return trav_init<true, kCount>(sc, T, P, dir, 0.0f, 0.001f, tmax, key, info >> 8,
+    return trav_init<true, kCount>(sc, T, S, P, dir, 0.0f, 0.001f, tmax, key, info >> 8,
                                    rr == 0 ? DOM_VOL_SH_HDRI : DOM_VOL_SH_AREA, cnt);
   };
   // ray r of the current job ended with status s; true when the job is done
@@ -481,11 +505,11 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES) void k_shadow(DScene sc, WaveA
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE, Q, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
-      pn = idx;
-      qp = a.sj_p[idx];
-      qa = a.sj_a[idx];
-      if (kEnvIS) qh = a.sj_h[idx];
-      if (kEnvIS || kVol) qinfo = a.sj_info[idx];
+      pn = GIX(idx, a.slots, 46);
+      qp = a.sj_p[pn];
+      qa = a.sj_a[pn];
+      if (kEnvIS) qh = a.sj_h[pn];
+      if (kEnvIS || kVol) qinfo = a.sj_info[pn];
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (Q.dry) break;
@@ -512,7 +536,7 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
     if ((flags & 2u) && (vis & 2u)) { const float4 eh = a.ne_h[k]; direct = add(direct, mk(eh.x, eh.y, eh.z)); }
     if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
     const uint32_t t = asu(ea.w);
-    float4* Lp = (t & TARGET_SLOT) ? a.Lout + (t & ~TARGET_SLOT) : Lnext + t;
+    float4* Lp = (t & TARGET_SLOT) ? a.Lout + GIX(t & ~TARGET_SLOT, a.slots, 47) : Lnext + GIX(t, a.slots, 48);
     const float4 L4 = *Lp;
     const V3 L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
     *Lp = make_float4(L.x, L.y, L.z, L4.w);
@@ -553,6 +577,9 @@ __global__ void k_count_samples(WaveArgs a, uint32_t n) {
 }
 
 // ---------------------------------------------------------------- host side
+// (left out of the test-only host emulation, tests/wave_emu.cpp, which drives
+// the kernels above itself)
+#ifndef RTG_HOST_EMU
 static int grid_for(const void* fn, int block, size_t lds, uint32_t items, int cus) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds) != hipSuccess || per_cu < 1) per_cu = 1;
@@ -595,6 +622,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
     const int gap = grid_for((const void*)k_nee_apply, 256, 0, nslots, cus);
     for (int b = 0; b < plan.max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
+#ifdef RTG_GUARD
+      // poison the hit records: k_shade reports any that k_extend did not write
+      if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
+#endif
       if ((e = mark(plan, KC_EXTEND, st)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, a.s[c], cnt_stream[c],
                          cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext);
@@ -655,5 +686,6 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
                        st, a, out, accumulate);
   return hipGetLastError();
 }
+#endif  // RTG_HOST_EMU
 
 }  // namespace rtg

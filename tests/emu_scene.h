@@ -1,0 +1,82 @@
+// emu_scene.h — test-only: build a librtscene scene, flatten it with
+// flatten.cpp and expose it as the kernels' DScene / DCamera over host
+// vectors (the host emulations tests/trav_emu.cpp and tests/wave_emu.cpp).
+#pragma once
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../go-raytracing_amd/csrc/dev_layout.h"
+#include "../go-raytracing_amd/csrc/flatten.h"
+#include "../include/rtscene.h"
+
+namespace emu {
+
+using namespace rtg;
+
+template <class T>
+static const T* ptr(const std::vector<T>& v) { return v.empty() ? nullptr : v.data(); }
+
+struct EmuScene {
+  rts_scene* scn = nullptr;
+  HostScene h;
+  DScene d{};
+  DCamera cam{};
+  int max_depth = 0;
+  ~EmuScene() { if (scn) rts_scene_destroy(scn); }
+};
+
+// Returns 0 on success, else an exit code (message on stderr).
+static int load(const char* name, int width, const char* asset_dir, EmuScene& E) {
+  rts_scene_options opt{};
+  opt.width = width;
+  opt.lucy_rings = 60;
+  opt.lucy_cols = 80;
+  opt.asset_dir = asset_dir;
+  char err[512] = {0};
+  if (rts_scene_create(name, &opt, &E.scn, err, sizeof err) != 0) { fprintf(stderr, "%s\n", err); return 3; }
+  std::string ferr;
+  if (flatten_scene(rts_scene_get_desc(E.scn), E.h, ferr)) { fprintf(stderr, "%s\n", ferr.c_str()); return 4; }
+  const HostScene& h = E.h;
+  DScene& d = E.d;
+  d.nodes = ptr(h.nodes4); d.leaves = ptr(h.leaves); d.refs = ptr(h.refs); d.ref_rank = ptr(h.ref_rank);
+  d.ref_box = ptr(h.ref_box); d.spheres = ptr(h.spheres); d.quads = ptr(h.quads); d.tris = ptr(h.tris);
+  d.tri_aux = ptr(h.tri_aux); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
+  d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
+  d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
+  d.tri_rank = ptr(h.tri_rank); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);
+  d.quad_hidx = ptr(h.quad_hidx); d.tri_hidx = ptr(h.tri_hidx); d.plane_hidx = ptr(h.plane_hidx);
+  d.volume_hidx = ptr(h.volume_hidx);
+  d.tlas = h.tlas;
+  d.env.valid = h.env_valid; d.env.width = h.env_w; d.env.height = h.env_h; d.env.use_is = h.env_use_is;
+  d.env.rotation = h.env_rotation; d.env.total_power = h.env_total_power;
+  d.env.texels = ptr(h.env_texels); d.env.pdf = ptr(h.env_pdf); d.env.marginal = ptr(h.env_marginal);
+  d.env.conditional = ptr(h.env_conditional);
+  d.num_planes = int(h.planes.size()); d.num_lights = int(h.lights.size());
+  d.num_materials = int(h.materials.size()); d.num_textures = int(h.textures.size());
+  d.stack_needed = h.stack_needed; d.has_volumes = h.volumes.empty() ? 0 : 1;
+  d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
+  d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
+  d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
+  d.n_volumes = uint32_t(h.volumes.size());
+  d.has_fancy = 0;
+  for (const DMaterial& m : h.materials)
+    if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
+
+  const rt_camera_desc* c = rts_scene_get_camera(E.scn);
+  DCamera& cam = E.cam;
+  for (int a = 0; a < 3; ++a) {
+    cam.center[a] = float(c->center[a]); cam.pixel00[a] = float(c->pixel00[a]);
+    cam.du[a] = float(c->pixel_delta_u[a]); cam.dv[a] = float(c->pixel_delta_v[a]);
+    cam.disk_u[a] = float(c->defocus_disk_u[a]); cam.disk_v[a] = float(c->defocus_disk_v[a]);
+    cam.background[a] = float(c->background[a]);
+  }
+  cam.defocus = c->defocus_angle > 0.0 ? 1 : 0; cam.use_sky = c->use_sky_gradient ? 1 : 0;
+  cam.phantom = c->phantom_hdri ? 1 : 0; cam.cam_max_depth = c->max_depth;
+  cam.width = c->image_width; cam.height = c->image_height;
+  E.max_depth = c->max_depth;
+  return 0;
+}
+
+}  // namespace emu

@@ -9,6 +9,12 @@
   wave-mates in the while-while vote, run under AddressSanitizer +
   UBSan, and compared with the oracle's fp32 mode (same op order): the
   per-pixel sums agree to fp32 accumulation rounding.
+* tests/wave_emu.cpp: the production wavefront kernels (wavefront.hip:
+  camera, extend, shade, shadow, NEE apply, accumulate) compiled for the
+  host, one lane per workgroup, driven batch by batch like run_batches()
+  over exactly-sized buffers under AddressSanitizer + UBSan (every stream,
+  job and queue index checked), with a 4-entry stack ring (spill path) and a
+  non-identity pixel list; compared with the oracle's fp32 mode.
 """
 import json
 import os
@@ -42,6 +48,12 @@ def _build(tmp, src, out, sanitize=False):
 def probe(tmp_path_factory, g):
     t = tmp_path_factory.mktemp("probe")
     return _build(t, "flatten_probe.cpp", t / "probe")
+
+
+@pytest.fixture(scope="module")
+def wave(tmp_path_factory, g):
+    t = tmp_path_factory.mktemp("wave")
+    return _build(t, "wave_emu.cpp", t / "wave", sanitize=True)
 
 
 @pytest.fixture(scope="module")
@@ -83,4 +95,24 @@ def test_device_source_under_asan_matches_oracle(emu, O, g, tmp_path, name):
     ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
     got = np.fromfile(out, np.float32).reshape(ref.shape)
     # same op order: only the fp32 rounding of the per-pixel sum differs
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())
+
+
+@pytest.mark.parametrize("name,batch", [("simple", 0), ("cornell", 1), ("cornell-smoke", 0), ("cornell-lucy", 1),
+                                        ("hdri-nee", 0), ("random", 0)])
+def test_wavefront_kernels_under_asan_match_oracle(wave, O, g, tmp_path, name, batch):
+    spp, seed, width = 2, 77, 40
+    out = tmp_path / f"{name}.f32"
+    args = [wave, name, str(width), str(spp), str(seed), ASSETS, str(out)]
+    if batch:
+        args.append(str(batch))   # one sample per batch: several batches
+    r = subprocess.run(args, capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    kw = dict(width=width)
+    if name == "cornell-lucy":
+        kw.update(lucy_rings=60, lucy_cols=80)
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
+    got = np.fromfile(out, np.float32).reshape(ref.shape)
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())

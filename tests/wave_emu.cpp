@@ -1,0 +1,118 @@
+// wave_emu.cpp — test-only host build of the production wavefront pipeline
+// (go-raytracing_amd/csrc/wavefront.hip kernels: camera, extend, shade,
+// shadow, NEE apply, accumulate, finalize) with one lane per workgroup and
+// one workgroup per launch, driven like run_batches() over a librtscene scene
+// flattened by flatten.cpp.  Runs under AddressSanitizer + UBSan in the CPU
+// suite (tests/test_flatten_host.py): every stream / queue / job index the
+// kernels compute is checked against exactly-sized host buffers.  The
+// traversal stack ring is 4 entries so deep traversals take the spill path.
+// Not a product path: the product is the gfx950 build in librtgpu.so.
+//
+// usage: wave_emu <scene> <width> <spp> <seed> <asset_dir> <out.f32> [batch_spp]
+// writes H*W*3 float sums (the accumulation buffer rt_render returns).
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../go-raytracing_amd/csrc/wavefront.hip"
+#include "emu_scene.h"
+
+using namespace rtg;
+
+namespace {
+
+constexpr int kRing = 4;
+
+template <bool kVol, bool kEnvIS, bool kFancy>
+void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_t spb, int max_depth, float* out) {
+  uint32_t* cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
+  uint32_t* cnt_shadow = a.counts + CNT_SHADOW;
+  uint32_t* fetch_ext = a.counts + CNT_FETCH_EXT;
+  uint32_t* fetch_sh = a.counts + CNT_FETCH_SH;
+  for (double* p = a.acc; p < a.acc + size_t(a.npix) * 3; ++p) *p = 0.0;
+  for (uint32_t s0 = 0; s0 < spp; s0 += spb) {
+    const uint32_t sb = spp - s0 < spb ? spp - s0 : spb;
+    const uint32_t nslots = sb * a.npix;
+    k_set_counts(a.counts, nslots);
+    k_camera(cam, a, a.s[0], nslots, s0);
+    for (int b = 0; b < max_depth; ++b) {
+      const int c = b & 1, nx = c ^ 1;
+      k_extend<kRing, false, kVol>(sc, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext);
+      k_shade<false, kEnvIS, kFancy>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx]);
+      k_shadow<kRing, false, kVol, kEnvIS>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
+      k_nee_apply(a, cnt_shadow, a.s[nx].L);
+    }
+    k_accum(a, sb);
+  }
+  k_finalize(a, out, 0);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 7) return 2;
+  const uint32_t spp = uint32_t(atoi(argv[3]));
+  const uint32_t seed = uint32_t(strtoul(argv[4], nullptr, 10));
+  const uint32_t spb = argc > 7 ? uint32_t(atoi(argv[7])) : spp;
+  emu::EmuScene E;
+  if (int rc = emu::load(argv[1], atoi(argv[2]), argv[5], E)) return rc;
+  const DScene& d = E.d;
+  const DCamera& cam = E.cam;
+  const uint32_t npix = uint32_t(cam.width) * uint32_t(cam.height);
+  const size_t S = size_t(spb) * npix;
+
+  // exactly-sized buffers (the layout of render_wave in api.cpp)
+  std::vector<float4> f4(16 * S, float4{0.0f, 0.0f, 0.0f, 0.0f});
+  std::vector<uint32_t> q(CNT_WORDS_Q + 2 * S, 0u);
+  std::vector<uint32_t> pixels(npix);
+  // bucket-like pixel list: reversed, so slot -> pixel is not the identity
+  for (uint32_t i = 0; i < npix; ++i) pixels[i] = npix - 1u - i;
+  std::vector<uint32_t> spill(size_t(kStackMax - kRing), 0u);
+  std::vector<double> acc(size_t(npix) * 3, 0.0);
+  std::vector<unsigned long long> counters(3 * CNT_BLOCK, 0ull);
+  int err = 0;
+
+  WaveArgs a{};
+  float4* base = f4.data();
+  for (int k = 0; k < 2; ++k) {
+    float4* sb = base + size_t(4 * k) * S;
+    a.s[k] = PathStream{sb, sb + S, sb + 2 * S, sb + 3 * S};
+  }
+  a.hit = base + 8 * S; a.Lout = base + 9 * S;
+  a.sj_p = base + 10 * S; a.sj_a = base + 11 * S; a.sj_h = base + 12 * S;
+  a.ne_a = base + 13 * S; a.ne_h = base + 14 * S; a.ne_beta = base + 15 * S;
+  a.counts = q.data();
+  a.sj_info = q.data() + CNT_WORDS_Q;
+  a.sj_vis = a.sj_info + S;
+  a.pixels = pixels.data();
+  a.npix = npix;
+  a.acc = acc.data();
+  a.seed = seed;
+  a.max_depth = E.max_depth;
+  a.counters = counters.data();
+  a.err = &err;
+  a.refill = 1;                      // one lane per wave: claim whenever idle
+  a.spill = spill.data();
+  a.spill_lanes = 1;
+  a.spill_cap = kStackMax - kRing;
+  a.slots = uint32_t(S);
+
+  std::vector<float> out(size_t(npix) * 3, 0.0f);
+  const bool vol = d.has_volumes != 0, envis = d.env.valid && d.env.use_is, fancy = d.has_fancy != 0;
+#define RUN(V, H, F) run<V, H, F>(d, cam, a, spp, spb, E.max_depth, out.data())
+  if (vol) {
+    if (envis) { if (fancy) RUN(true, true, true); else RUN(true, true, false); }
+    else { if (fancy) RUN(true, false, true); else RUN(true, false, false); }
+  } else {
+    if (envis) { if (fancy) RUN(false, true, true); else RUN(false, true, false); }
+    else { if (fancy) RUN(false, false, true); else RUN(false, false, false); }
+  }
+#undef RUN
+  FILE* f = fopen(argv[6], "wb");
+  if (!f) return 5;
+  fwrite(out.data(), sizeof(float), out.size(), f);
+  fclose(f);
+  printf("{\"width\": %d, \"height\": %d, \"slots\": %zu, \"overflow\": %d}\n", cam.width, cam.height, S, err);
+  return err ? 6 : 0;
+}
