@@ -280,9 +280,10 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     plan.max_events = int(ctx->tev.size());
     plan.num_events = &ctx->tev_used;
   }
-  // LDS stack ring (16 or 32 entries per lane, RTGPU_STACK) + global spill
+  // LDS stack ring (8 entries per lane by default, 16 with RTGPU_STACK=16) +
+  // global spill
   // up to kStackMax: scenes of any supported depth run with the small ring.
-  static const int lds_stack = [] { const char* e = getenv("RTGPU_STACK"); return e && atoi(e) == 32 ? 32 : 16; }();
+  static const int lds_stack = [] { const char* e = getenv("RTGPU_STACK"); return e && atoi(e) == 16 ? 16 : 8; }();
   const int stack = lds_stack;
   a.spill_lanes = uint32_t(std::max(1, ctx->num_cus)) * kSpillLanesPerCU;
   a.spill_cap = kStackMax - stack;

@@ -26,12 +26,12 @@
 #include "wavefront.h"
 
 // Minimum waves per SIMD requested for the traversal kernels (register cap:
-// 6 waves = 80 VGPRs; the LDS ring + world ray, 25.6 KB per block, also
-// allows 6).  The traversal is latency- and issue-bound; measured on
-// CornellBoxLucy with the world ray in LDS: 5 waves 681, 6 waves 745
-// Msamples/s (1-3 VGPRs spilled).
+// 7 waves = 72 VGPRs).  The traversal is latency- and issue-bound, so
+// occupancy pays; measured on CornellBoxLucy (Msamples/s): 5 waves / 16-entry
+// LDS ring 681, 6 / 16 745, 7 / 8 757, 8 / 8 756 (64 B/lane of spills).  The
+// 8-entry ring + world ray (17 KB per block) lets LDS allow 9 blocks per CU.
 #ifndef RTG_TRAV_WAVES
-#define RTG_TRAV_WAVES 6
+#define RTG_TRAV_WAVES 7
 #endif
 // The volume (fog) and instrumented variants carry more live state: at the
 // 96-VGPR cap they spill 40-120 VGPRs to scratch, so they keep 4 waves
@@ -671,12 +671,12 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     }                                                                             \
   } while (0)
     const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0;
-    if (stack <= 16) {
+    if (stack > 8) {
       if (vol) { if (count) RUN(16, true, true); else RUN(16, false, true); }
       else { if (count) RUN(16, true, false); else RUN(16, false, false); }
     } else {
-      if (vol) { if (count) RUN(32, true, true); else RUN(32, false, true); }
-      else { if (count) RUN(32, true, false); else RUN(32, false, false); }
+      if (vol) { if (count) RUN(8, true, true); else RUN(8, false, true); }
+      else { if (count) RUN(8, true, false); else RUN(8, false, false); }
     }
 #undef RUN
     if (e != hipSuccess) return e;
