@@ -46,7 +46,7 @@ try:
 except Exception:
     pass
 cfg = bench.get("config", {})
-out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --spp 100",
+out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --steps 1 --warmup 0 (default workload: the timed steps' per-launch batches)",
        "scene": cfg.get("scene", "cornell-lucy"), "width": cfg.get("width"), "height": cfg.get("height"),
        "kernels": {}}
 for fam, v in vals.items():
