@@ -184,10 +184,12 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
       for (int x = t.x; x < t.x + t.z; ++x) px.push_back(uint32_t(y) * uint32_t(dc.width) + uint32_t(x));
   const uint32_t npix = uint32_t(px.size());
   const uint32_t spp = uint32_t(p->samples_per_pixel);
-  // Path slots per batch: as many as fit in a quarter of the free HBM, up to
-  // 128M (larger batches amortise each launch's ramp-down tail; measured on
-  // CornellBoxLucy: 4M slots 330, 64M slots 444 Msamples/s).  Samples are
-  // split evenly over the batches.  RTGPU_SLOTS overrides (tuning knob).
+  // Path slots per batch: as many as fit in half the free HBM, up to 512M
+  // (135 GB at 264 B per slot).  Larger batches amortise every launch's
+  // ramp-down tail; measured on CornellBoxLucy (Msamples/s): 8M slots 501,
+  // 32M 686, 128M 759, 210M 799, the whole 405M-sample frame in one batch
+  // 833.  Samples are split evenly over the batches.  RTGPU_SLOTS overrides
+  // (tuning knob).
   // Per slot: two path streams (4 x 16 B each), hit, Lout, six NEE job
   // fields (16 B each), job info + visibility words.
   constexpr size_t kSlotF4 = 16;
@@ -201,7 +203,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = size_t(8) << 30;
     free_b += ctx->wslots * kSlotBytes;   // the current batch buffers can be reused
-    target = std::min<size_t>(size_t(128) << 20, std::max<size_t>(size_t(1) << 20, free_b / 4 / kSlotBytes));
+    target = std::min<size_t>(size_t(512) << 20, std::max<size_t>(size_t(1) << 20, free_b / 2 / kSlotBytes));
   }
   const uint32_t max_spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
   const uint32_t nbatch = (spp + max_spb - 1) / max_spb;
