@@ -49,6 +49,28 @@ namespace rtg {
 __device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t asu(float f) { return __float_as_uint(f); }
 
+// Path-stream accesses: every stream / job element is touched once per
+// bounce, so they are non-temporal (no reuse to keep in L2 / the Infinity
+// Cache, which then holds the BVH and primitives the traversal re-reads).
+#ifdef RTG_HOST_EMU
+__device__ __forceinline__ float4 ldnt(const float4* p) { return *p; }
+__device__ __forceinline__ void stnt(float4* p, float4 v) { *p = v; }
+__device__ __forceinline__ uint32_t ldnt(const uint32_t* p) { return *p; }
+__device__ __forceinline__ void stnt(uint32_t* p, uint32_t v) { *p = v; }
+#else
+typedef float rtg_v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldnt(const float4* p) {
+  const rtg_v4f v = __builtin_nontemporal_load(reinterpret_cast<const rtg_v4f*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stnt(float4* p, float4 v) {
+  rtg_v4f w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<rtg_v4f*>(p));
+}
+__device__ __forceinline__ uint32_t ldnt(const uint32_t* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void stnt(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+#endif
+
 // path state word: depth_left (16) | bounce (15) << 16 | allow << 31
 __device__ __forceinline__ uint32_t pack_state(int depth, uint32_t bounce, bool allow) {
   return uint32_t(depth & 0xFFFF) | ((bounce & 0x7FFFu) << 16) | (allow ? 0x80000000u : 0u);
@@ -99,10 +121,10 @@ __global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, PathStr
       ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
     }
     V3 rd = sub(ps, ro);
-    s.o[i] = make_float4(ro.x, ro.y, ro.z, time);
-    s.d[i] = make_float4(rd.x, rd.y, rd.z, asf(key));
-    s.beta[i] = make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true)));
-    s.L[i] = make_float4(0.0f, 0.0f, 0.0f, asf(i));
+    stnt(&s.o[i], make_float4(ro.x, ro.y, ro.z, time));
+    stnt(&s.d[i], make_float4(rd.x, rd.y, rd.z, asf(key)));
+    stnt(&s.beta[i], make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true))));
+    stnt(&s.L[i], make_float4(0.0f, 0.0f, 0.0f, asf(i)));
   }
 }
 
@@ -145,8 +167,8 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
 
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
-  hit[p] = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
-                       0.0f);
+  stnt(&hit[p], make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
+                       0.0f));
 }
 
 // ---------------------------------------------------------------- extend
@@ -183,9 +205,9 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
     const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
       pn = GIX(idx, a.slots, 40);
-      po = cs.o[pn];
-      pd = cs.d[pn];
-      if (kVol) pb = (asu(cs.beta[pn].w) >> 16) & 0x7FFFu;
+      po = ldnt(&cs.o[pn]);
+      pd = ldnt(&cs.d[pn]);
+      if (kVol) pb = (asu(ldnt(&cs.beta[pn]).w) >> 16) & 0x7FFFu;
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (P.dry) break;
@@ -262,7 +284,8 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
     V3 L = mk(0.0f, 0.0f, 0.0f), P = L, sd = L, beta = L, nbeta = L, ca = L, ch = L, da = L, dh = L;
     if (live) {
       const uint32_t ii = GIX(i, a.slots, 41);
-      const float4 h = a.hit[ii], o4 = cs.o[ii], d4 = cs.d[ii], b4 = cs.beta[ii], L4 = cs.L[ii];
+      const float4 h = ldnt(&a.hit[ii]), o4 = ldnt(&cs.o[ii]), d4 = ldnt(&cs.d[ii]), b4 = ldnt(&cs.beta[ii]),
+                   L4 = ldnt(&cs.L[ii]);
       key = asu(d4.w);
       slot = asu(L4.w);
       const uint32_t st = asu(b4.w);
@@ -418,23 +441,23 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
     block_reserve2(cont, want_shadow, ncount, a.counts + CNT_SHADOW, s_w[par], s_b[par], jc, js);
     if (cont) {
       jc = GIX(jc, a.slots, 43);
-      ns.o[jc] = make_float4(P.x, P.y, P.z, time);
-      ns.d[jc] = make_float4(sd.x, sd.y, sd.z, asf(key));
-      ns.beta[jc] = make_float4(nbeta.x, nbeta.y, nbeta.z, asf(nstate));
-      ns.L[jc] = make_float4(L.x, L.y, L.z, asf(slot));
+      stnt(&ns.o[jc], make_float4(P.x, P.y, P.z, time));
+      stnt(&ns.d[jc], make_float4(sd.x, sd.y, sd.z, asf(key)));
+      stnt(&ns.beta[jc], make_float4(nbeta.x, nbeta.y, nbeta.z, asf(nstate)));
+      stnt(&ns.L[jc], make_float4(L.x, L.y, L.z, asf(slot)));
     } else if (live) {
       slot = GIX(slot, a.slots, 44);
-      a.Lout[slot] = make_float4(L.x, L.y, L.z, 0.0f);
+      stnt(&a.Lout[slot], make_float4(L.x, L.y, L.z, 0.0f));
     }
     if (want_shadow) {
       js = GIX(js, a.slots, 45);
-      a.sj_p[js] = make_float4(P.x, P.y, P.z, asf(key));
-      a.sj_a[js] = make_float4(da.x, da.y, da.z, tmax_a);
-      if (kEnvIS) a.sj_h[js] = make_float4(dh.x, dh.y, dh.z, 0.0f);
-      a.sj_info[js] = flags | (bounce << 8);
-      a.ne_a[js] = make_float4(ca.x, ca.y, ca.z, asf(cont ? jc : (slot | TARGET_SLOT)));
-      if (kEnvIS) a.ne_h[js] = make_float4(ch.x, ch.y, ch.z, 0.0f);
-      a.ne_beta[js] = make_float4(beta.x, beta.y, beta.z, 0.0f);
+      stnt(&a.sj_p[js], make_float4(P.x, P.y, P.z, asf(key)));
+      stnt(&a.sj_a[js], make_float4(da.x, da.y, da.z, tmax_a));
+      if (kEnvIS) stnt(&a.sj_h[js], make_float4(dh.x, dh.y, dh.z, 0.0f));
+      stnt(&a.sj_info[js], flags | (bounce << 8));
+      stnt(&a.ne_a[js], make_float4(ca.x, ca.y, ca.z, asf(cont ? jc : (slot | TARGET_SLOT))));
+      if (kEnvIS) stnt(&a.ne_h[js], make_float4(ch.x, ch.y, ch.z, 0.0f));
+      stnt(&a.ne_beta[js], make_float4(beta.x, beta.y, beta.z, 0.0f));
     }
   }
   if (kCount) add_counters(a.counters + KC_SHADE * CNT_BLOCK, cnt, 0);
@@ -481,7 +504,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_shado
       if (s2 == TRAV_RUNNING) return false;
       if (s2 != TRAV_ANYHIT) vis |= 1u;
     }
-    a.sj_vis[p] = vis;
+    stnt(&a.sj_vis[p], vis);
     return true;
   };
   for (;;) {
@@ -506,10 +529,10 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_shado
     const uint32_t idx = pool_take(pn == ITEM_NONE, Q, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
       pn = GIX(idx, a.slots, 46);
-      qp = a.sj_p[pn];
-      qa = a.sj_a[pn];
-      if (kEnvIS) qh = a.sj_h[pn];
-      if (kEnvIS || kVol) qinfo = a.sj_info[pn];
+      qp = ldnt(&a.sj_p[pn]);
+      qa = ldnt(&a.sj_a[pn]);
+      if (kEnvIS) qh = ldnt(&a.sj_h[pn]);
+      if (kEnvIS || kVol) qinfo = ldnt(&a.sj_info[pn]);
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (Q.dry) break;
@@ -530,10 +553,10 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
-    const uint32_t flags = a.sj_info[k] & 0xFFu, vis = a.sj_vis[k];
-    const float4 ea = a.ne_a[k], pb = a.ne_beta[k];
+    const uint32_t flags = ldnt(&a.sj_info[k]) & 0xFFu, vis = ldnt(&a.sj_vis[k]);
+    const float4 ea = ldnt(&a.ne_a[k]), pb = ldnt(&a.ne_beta[k]);
     V3 direct = mk(0.0f, 0.0f, 0.0f);
-    if ((flags & 2u) && (vis & 2u)) { const float4 eh = a.ne_h[k]; direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+    if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
     if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
     const uint32_t t = asu(ea.w);
     float4* Lp = (t & TARGET_SLOT) ? a.Lout + GIX(t & ~TARGET_SLOT, a.slots, 47) : Lnext + GIX(t, a.slots, 48);
@@ -549,7 +572,7 @@ __global__ __launch_bounds__(256) void k_accum(WaveArgs a, uint32_t nsamp) {
   for (uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x; pi < a.npix; pi += gs) {
     double sx = a.acc[size_t(pi) * 3], sy = a.acc[size_t(pi) * 3 + 1], sz = a.acc[size_t(pi) * 3 + 2];
     for (uint32_t s = 0; s < nsamp; ++s) {
-      const float4 L = a.Lout[size_t(s) * a.npix + pi];
+      const float4 L = ldnt(&a.Lout[size_t(s) * a.npix + pi]);
       sx += double(L.x); sy += double(L.y); sz += double(L.z);
     }
     a.acc[size_t(pi) * 3] = sx; a.acc[size_t(pi) * 3 + 1] = sy; a.acc[size_t(pi) * 3 + 2] = sz;
