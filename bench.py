@@ -64,8 +64,9 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=0, help="0: scene default")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--blas", choices=["sah", "reference"], default="sah",
-                    help="BVH layout (mesh BLAS and world BVH): SAH (default) or the caller's topology")
+    ap.add_argument("--blas", choices=["sah", "reference", "device"], default="sah",
+                    help="mesh BLAS builder: host SAH (default), the caller's topology, or the GPU LBVH "
+                         "(build.hip); the world BVH is SAH except for 'reference'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented count run")
     ap.add_argument("--cpu-spp", type=int, default=48, help="spp of the CPU baseline sample")
@@ -108,7 +109,7 @@ def main():
     W, H, spp, depth = cam.image_width, cam.image_height, cam.samples_per_pixel, cam.max_depth
     ctx = g.Context(local if world > 1 else 0)
     ctx.set_blas_builder(args.blas)
-    ctx.set_tlas_builder(args.blas)
+    ctx.set_tlas_builder("reference" if args.blas == "reference" else "sah")
     ctx.upload(scene.desc)
     info = ctx.info()
     t_build = time.time() - t_build
@@ -225,7 +226,8 @@ def main():
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "parallelism": f"tiles-rr{world}", "buckets": len(buckets), "blas": args.blas,
                        "triangles": info.triangles, "bvh_nodes": info.nodes,
-                       "scene_build_s": round(t_build, 2), "image_finite": img_ok},
+                       "scene_build_s": round(t_build, 2), "device_bvh_build_ms": round(ctx.last_build_ms(), 2),
+                       "image_finite": img_ok},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

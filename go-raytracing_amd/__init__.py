@@ -29,7 +29,7 @@ ASSET_DIR = os.path.join(REPO_DIR, "assets")
 
 RT_OK = 0
 RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER = 1, 2
-RT_BLAS_REFERENCE, RT_BLAS_SAH = 0, 1
+RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_SCENE", -6: "RT_ERR_DEVICE"}
 
@@ -143,6 +143,7 @@ def rtgpu() -> C.CDLL:
         lib.rt_last_error.restype = C.c_char_p
         lib.rt_scene_upload.argtypes = [P, C.POINTER(RtSceneDesc)]
         lib.rt_scene_get_info.argtypes = [P, C.POINTER(RtSceneInfo)]
+        lib.rt_last_build_ms.argtypes = [P, C.POINTER(C.c_double)]
         lib.rt_render.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), C.POINTER(C.c_float),
                                   C.POINTER(RtStats)]
         lib.rt_render_device.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), P, P]
@@ -382,8 +383,16 @@ class Context:
         self._check(self._lib.rt_ctx_set_option(self._h, key, value))
 
     def set_blas_builder(self, builder: str):
-        """Mesh BLAS layout: "sah" (default) or "reference" (the caller's BVH topology); next upload."""
-        self.set_option(RT_OPT_BLAS_BUILDER, {"reference": RT_BLAS_REFERENCE, "sah": RT_BLAS_SAH}[builder])
+        """Mesh BLAS layout, next upload: "sah" (default, host binned SAH), "reference" (the
+        caller's BVH topology) or "device" (LBVH built on the GPU, build.hip)."""
+        self.set_option(RT_OPT_BLAS_BUILDER,
+                        {"reference": RT_BLAS_REFERENCE, "sah": RT_BLAS_SAH, "device": RT_BLAS_DEVICE}[builder])
+
+    def last_build_ms(self) -> float:
+        """Wall time of the device BVH builds of the last upload (0 for host-built BLASes)."""
+        ms = C.c_double()
+        self._check(self._lib.rt_last_build_ms(self._h, C.byref(ms)))
+        return ms.value
 
     def set_tlas_builder(self, builder: str):
         """World BVH layout: "sah" (default) or "reference"; next upload."""

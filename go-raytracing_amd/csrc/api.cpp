@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -14,6 +15,7 @@
 
 #include "../../include/rtgpu.h"
 #include "dev_layout.h"
+#include "build.h"
 #include "flatten.h"
 #include "render_launch.h"
 #include "wavefront.h"
@@ -57,6 +59,9 @@ struct rt_ctx {
   std::vector<uint8_t> tev_class;
   int tev_used = 0;
   FlattenOptions fopt;
+  // device BVH build (RT_BLAS_DEVICE) of the last upload
+  uint32_t dev_nodes = 0, dev_leaves = 0;   // nodes / leaves added on the device
+  double build_ms = 0.0;                    // wall time of the device builds
 };
 
 namespace {
@@ -90,10 +95,11 @@ int ensure(rt_ctx* ctx, DevBuf& b, size_t bytes) {
   return RT_OK;
 }
 
+// Copies `v` to a new device buffer with room for `extra` more elements.
 template <typename T>
-int upload_vec(rt_ctx* ctx, const std::vector<T>& v, const T** dst) {
+int upload_vec(rt_ctx* ctx, const std::vector<T>& v, const T** dst, size_t extra = 0) {
   DevBuf b;
-  size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  size_t bytes = std::max<size_t>((v.size() + extra) * sizeof(T), 16);
   hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scene)");
   b.bytes = bytes;
@@ -450,8 +456,9 @@ const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->error.c_str() :
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (!ctx) return RT_ERR_INVALID;
   if (key == RT_OPT_BLAS_BUILDER) {
-    if (value != RT_BLAS_REFERENCE && value != RT_BLAS_SAH) return set_err(ctx, RT_ERR_INVALID, "bad BLAS builder");
-    ctx->fopt.blas_builder = value == RT_BLAS_SAH ? BLAS_SAH : BLAS_REFERENCE;
+    if (value != RT_BLAS_REFERENCE && value != RT_BLAS_SAH && value != RT_BLAS_DEVICE)
+      return set_err(ctx, RT_ERR_INVALID, "bad BLAS builder");
+    ctx->fopt.blas_builder = value == RT_BLAS_SAH ? BLAS_SAH : value == RT_BLAS_DEVICE ? BLAS_DEVICE : BLAS_REFERENCE;
     return RT_OK;
   }
   if (key == RT_OPT_TLAS_BUILDER) {
@@ -460,6 +467,54 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
     return RT_OK;
   }
   return set_err(ctx, RT_ERR_INVALID, "unknown option " + std::to_string(key));
+}
+
+// RT_BLAS_DEVICE: build every queued mesh BLAS on the device (build.hip),
+// point its header at the new root and redo the stack bound.
+static int device_builds(rt_ctx* ctx) {
+  HostScene& h = ctx->host;
+  DScene& d = ctx->dscene;
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t cap = 0;
+  for (const auto& j : h.device_builds) cap += j.n;
+  DeviceBuildTarget tgt{};
+  tgt.nodes = const_cast<DNode4*>(d.nodes);
+  tgt.nodes_used = uint32_t(h.nodes4.size());
+  tgt.nodes_cap = uint32_t(h.nodes4.size() + cap);
+  tgt.leaves = const_cast<DLeaf*>(d.leaves);
+  tgt.leaves_used = uint32_t(h.leaves.size());
+  tgt.leaves_cap = uint32_t(h.leaves.size() + cap);
+  tgt.tris = const_cast<DTri*>(d.tris);
+  tgt.tri_aux = const_cast<DTriAux*>(d.tri_aux);
+  tgt.tri_rank = const_cast<int32_t*>(d.tri_rank);
+  tgt.tri_hidx = const_cast<int32_t*>(d.tri_hidx);
+  int need = h.blas_need4;
+  for (const auto& j : h.device_builds) {
+    DevBuf boxes;
+    int rc = ensure(ctx, boxes, j.boxes.size() * sizeof(DRefBox));
+    if (rc) return rc;
+    hipError_t e = hipMemcpy(boxes.p, j.boxes.data(), j.boxes.size() * sizeof(DRefBox), hipMemcpyHostToDevice);
+    DeviceBuildJob job{j.blas, j.tri_first, j.n, {j.lo[0], j.lo[1], j.lo[2]}, {j.hi[0], j.hi[1], j.hi[2]}};
+    DeviceBuildResult res{};
+    if (e == hipSuccess) e = build_mesh_blas(job, static_cast<const DRefBox*>(boxes.p), tgt, res, ctx->stream);
+    free_buf(boxes);
+    if (e != hipSuccess) return hip_fail(ctx, e, "device BVH build");
+    tgt.nodes_used += res.nodes_added;
+    tgt.leaves_used += res.leaves_added;
+    ctx->dev_nodes += res.nodes_added;
+    ctx->dev_leaves += res.leaves_added;
+    need = std::max(need, res.need4);
+    h.blas[size_t(j.blas)].root_item = res.root_item;
+    HIPCHK(hipMemcpy(const_cast<DBvh*>(d.blas) + j.blas, &h.blas[size_t(j.blas)], sizeof(DBvh), hipMemcpyHostToDevice));
+  }
+  h.stack_needed = h.tlas_need4 + h.max_leaf_inst + 1 + need + 2;
+  if (h.stack_needed > kStackMax)
+    return set_err(ctx, RT_ERR_UNSUPPORTED, "device-built BVH too deep for the traversal stack");
+  d.stack_needed = h.stack_needed;
+  d.n_nodes = tgt.nodes_used;
+  d.n_leaves = tgt.leaves_used;
+  ctx->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return RT_OK;
 }
 
 int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
@@ -473,9 +528,11 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   HostScene& h = ctx->host;
   DScene& d = ctx->dscene;
   d = DScene{};
+  size_t dev_tris = 0;   // room for the device-built BLASes: < n nodes, <= n leaves each
+  for (const auto& j : h.device_builds) dev_tris += j.n;
 #define UP(vec, field) if ((rc = upload_vec(ctx, h.vec, &d.field))) { free_scene(ctx); return rc; }
-  UP(nodes4, nodes);
-  UP(leaves, leaves);
+  if ((rc = upload_vec(ctx, h.nodes4, &d.nodes, dev_tris))) { free_scene(ctx); return rc; }
+  if ((rc = upload_vec(ctx, h.leaves, &d.leaves, dev_tris))) { free_scene(ctx); return rc; }
   UP(refs, refs);
   UP(ref_rank, ref_rank);
   UP(ref_box, ref_box);
@@ -524,7 +581,16 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.has_fancy = 0;
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
+  ctx->dev_nodes = ctx->dev_leaves = 0;
+  ctx->build_ms = 0.0;
+  if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }
   ctx->has_scene = true;
+  return RT_OK;
+}
+
+int rt_last_build_ms(const rt_ctx* ctx, double* ms) {
+  if (!ctx || !ms) return RT_ERR_INVALID;
+  *ms = ctx->build_ms;
   return RT_OK;
 }
 
@@ -532,8 +598,8 @@ int rt_scene_get_info(const rt_ctx* ctx, rt_scene_info* o) {
   if (!ctx || !o) return RT_ERR_INVALID;
   if (!ctx->has_scene) return RT_ERR_NO_SCENE;
   const HostScene& h = ctx->host;
-  o->nodes = int(h.nodes4.size());   // device BVH4 nodes
-  o->leaves = int(h.leaves.size());
+  o->nodes = int(h.nodes4.size() + ctx->dev_nodes);   // device BVH4 nodes
+  o->leaves = int(h.leaves.size() + ctx->dev_leaves);
   o->refs = int(h.refs.size());
   o->spheres = int(h.spheres.size());
   o->quads = int(h.quads.size());

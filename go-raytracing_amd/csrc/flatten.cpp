@@ -397,7 +397,35 @@ struct Flattener {
     int depth = 0;
     blas_rank = 0;
     std::vector<int> mesh;
-    if (h.kind == RT_BVH_NODE && opt.blas_builder == BLAS_SAH && collect_triangles(g, mesh) &&
+    if (h.kind == RT_BVH_NODE && opt.blas_builder == BLAS_DEVICE && collect_triangles(g, mesh) &&
+        int(mesh.size()) >= opt.sah_min_prims) {
+      // Triangles in reference DFS order (tri_rank = DFS rank) + their boxes;
+      // the device builds the BVH at upload (build.hip).
+      HostScene::DeviceBuild job;
+      job.blas = int(S.blas.size());
+      job.tri_first = uint32_t(S.tris.size());
+      job.n = uint32_t(mesh.size());
+      Box all;
+      job.boxes.resize(mesh.size());
+      for (size_t i = 0; i < mesh.size(); ++i) {
+        const int ti = add_tri(mesh[i]);
+        S.tri_rank[ti] = int(i);
+        Box tb;
+        tb.merge(H(mesh[i]).bbox);
+        all.merge(tb);
+        float f[6];
+        store_box(f, tb);
+        DRefBox& rb = job.boxes[i];
+        rb.lo[0] = f[0]; rb.hi[0] = f[1]; rb.lo[1] = f[2]; rb.hi[1] = f[3]; rb.lo[2] = f[4]; rb.hi[2] = f[5];
+        rb.pad0 = rb.pad1 = 0.0f;
+      }
+      float f[6];
+      store_box(f, all);
+      job.lo[0] = f[0]; job.hi[0] = f[1]; job.lo[1] = f[2]; job.hi[1] = f[3]; job.lo[2] = f[4]; job.hi[2] = f[5];
+      S.device_builds.push_back(std::move(job));
+      b.root_item = empty_leaf;   // placeholder
+      b.check_box = 1;
+    } else if (h.kind == RT_BVH_NODE && opt.blas_builder == BLAS_SAH && collect_triangles(g, mesh) &&
         int(mesh.size()) >= opt.sah_min_prims) {
       // Same triangles, same closest hit (order-independent tie rule with
       // the reference DFS ranks), better tree: binned SAH.
@@ -1006,6 +1034,7 @@ struct Flattener {
     // stack: pending siblings along the worst world path + pending instances
     // in a leaf + the pending item and INST_END marker of an instance entry +
     // pending siblings along the worst BLAS path.
+    S.max_leaf_inst = max_leaf_inst;
     S.stack_needed = S.tlas_need4 + max_leaf_inst + 1 + S.blas_need4 + 2;
     if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
     if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27) || S.nodes4.size() >= (1u << 27))

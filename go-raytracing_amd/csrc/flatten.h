@@ -42,12 +42,24 @@ struct HostScene {
   int stack_needed = 0;
   int tlas_depth = 0, blas_depth = 0;   // BVH2 levels
   int tlas_need4 = 0, blas_need4 = 0;   // BVH4 stack entries along the worst root-to-leaf path
+  int max_leaf_inst = 0;                 // most instances in one world leaf (stack bound)
+  // Mesh BLASes left to the device builder (RT_BLAS_DEVICE): their triangles
+  // are in the arrays in reference DFS order; the BLAS header's root item is
+  // a placeholder until build_mesh_blas (build.hip) fills it in.
+  struct DeviceBuild {
+    int blas;
+    uint32_t tri_first, n;
+    float lo[3], hi[3];              // union of the triangle boxes
+    std::vector<DRefBox> boxes;      // per triangle: fp64 bbox rounded outward
+  };
+  std::vector<DeviceBuild> device_builds;
 };
 
 // How mesh BLASes are laid out (rt_ctx_set_option RT_OPT_BLAS_BUILDER).
 enum : int {
   BLAS_REFERENCE = 0,   // the caller's BVH topology (NewBVHNode, bvh.go:69-217)
   BLAS_SAH = 1,         // binned-SAH BVH2 over the same triangles (default)
+  BLAS_DEVICE = 2,      // LBVH built on the GPU at upload (build.hip)
 };
 struct FlattenOptions {
   int blas_builder = BLAS_SAH;

@@ -211,8 +211,10 @@ const char* rt_last_error(const rt_ctx* ctx);
  *   RT_OPT_BLAS_BUILDER: how an all-triangle mesh BVH (LoadOBJ ->
  *     NewBVHNode, obj_loader.go:109) is laid out on the device:
  *     RT_BLAS_REFERENCE = the caller's topology node for node;
- *     RT_BLAS_SAH (default) = binned-SAH BVH over the same triangles.
- *     Both give the same closest hit: the tie rule uses the reference's
+ *     RT_BLAS_SAH (default) = binned-SAH BVH over the same triangles;
+ *     RT_BLAS_DEVICE = LBVH built on the GPU during rt_scene_upload
+ *     (Morton sort + Karras hierarchy + refit + BVH4 collapse, build.hip).
+ *     All give the same closest hit: the tie rule uses the reference's
  *     DFS ranks, not the device visiting order.
  *   RT_OPT_TLAS_BUILDER: the world BVH (main.go:77 NewBVHNodeFromList):
  *     RT_BLAS_REFERENCE = the caller's topology; RT_BLAS_SAH (default) =
@@ -220,13 +222,17 @@ const char* rt_last_error(const rt_ctx* ctx);
  *     DFS rank and its leaf's test count (volumes).  Scenes holding a
  *     RotateX/RotateZ wrapper always keep the caller's topology.          */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2 };
-enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1 };
+enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);
 
 /* Flatten + upload the Go object graph (copied; caller memory not retained). */
 int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene);
 
 int rt_scene_get_info(const rt_ctx* ctx, rt_scene_info* out);
+
+/* Wall time (ms) of the device BVH builds (RT_BLAS_DEVICE) of the last
+ * rt_scene_upload on this context; 0 when every BLAS was built on the host. */
+int rt_last_build_ms(const rt_ctx* ctx, double* ms);
 
 /* Render the buckets into a caller-owned host buffer of width*height*3 float
  * (sum of per-sample radiance, linear).  Blocks until done.               */
