@@ -37,7 +37,7 @@ STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ER
 RT_SPHERE, RT_QUAD, RT_TRIANGLE, RT_PLANE, RT_LIST, RT_BVH_NODE, RT_BVH_LEAF = 1, 2, 3, 4, 5, 6, 7
 RT_TRANSLATE, RT_ROTATE_X, RT_ROTATE_Y, RT_ROTATE_Z, RT_SCALE, RT_VOLUME = 8, 9, 10, 11, 12, 13
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC, RT_DIFFUSE_LIGHT, RT_ISOTROPIC = 1, 2, 3, 4, 5
-RT_TEX_SOLID, RT_TEX_CHECKER = 1, 2
+RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_NOISE, RT_TEX_IMAGE = 1, 2, 3, 4
 
 
 class RtHittable(C.Structure):
@@ -52,7 +52,16 @@ class RtMaterial(C.Structure):
 
 class RtTexture(C.Structure):
     _fields_ = [("kind", C.c_int32), ("even", C.c_int32), ("odd", C.c_int32), ("albedo", C.c_double * 3),
-                ("inv_scale", C.c_double)]
+                ("inv_scale", C.c_double), ("scale", C.c_double), ("perlin", C.c_int32), ("image", C.c_int32)]
+
+
+class RtImage(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb", C.POINTER(C.c_double))]
+
+
+class RtPerlin(C.Structure):
+    _fields_ = [("randvec", (C.c_double * 3) * 256), ("perm_x", C.c_int32 * 256), ("perm_y", C.c_int32 * 256),
+                ("perm_z", C.c_int32 * 256)]
 
 
 class RtEnvironment(C.Structure):
@@ -66,7 +75,9 @@ class RtSceneDesc(C.Structure):
                 ("materials", C.POINTER(RtMaterial)), ("num_materials", C.c_int32),
                 ("textures", C.POINTER(RtTexture)), ("num_textures", C.c_int32),
                 ("lights", C.POINTER(C.c_int32)), ("num_lights", C.c_int32),
-                ("environment", C.POINTER(RtEnvironment))]
+                ("environment", C.POINTER(RtEnvironment)),
+                ("images", C.POINTER(RtImage)), ("num_images", C.c_int32),
+                ("perlins", C.POINTER(RtPerlin)), ("num_perlins", C.c_int32)]
 
 
 class RtCameraDesc(C.Structure):

@@ -556,6 +556,12 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(sphere_rank, sphere_rank);
   UP(quad_rank, quad_rank);
   UP(tri_rank, tri_rank);
+  UP(circles, circles);
+  UP(circle_rank, circle_rank);
+  UP(circle_hidx, circle_hidx);
+  UP(perlins, perlins);
+  UP(images, images);
+  UP(image_texels, image_texels);
   UP(env_texels, env.texels);
   UP(env_pdf, env.pdf);
   UP(env_marginal, env.marginal);
@@ -578,9 +584,13 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
   d.n_volumes = uint32_t(h.volumes.size());
+  d.n_circles = uint32_t(h.circles.size());
   d.has_fancy = 0;
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
+  d.needs_uv = 0;
+  for (const DTexture& t : h.textures)
+    if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;
   if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }

@@ -42,6 +42,7 @@ enum : int {
   PK_INSTANCE = 4,
   PK_VOLUME = 5,
   PK_PLANE = 6,   // only used in hit records
+  PK_CIRCLE = 7,
 };
 constexpr int REF_SHIFT = 28;
 constexpr uint32_t REF_MASK = (1u << REF_SHIFT) - 1u;
@@ -99,6 +100,12 @@ struct alignas(16) DQuad {     // quad.go:5-14
   float wx, wy, wz, pad2;
 };
 
+struct alignas(16) DCircle {   // circle.go:5-12
+  float cx, cy, cz, r;         // center, radius
+  float nx, ny, nz, D;         // unit normal, Dot(normal, center)
+  int32_t mat, pad0, pad1, pad2;
+};
+
 struct DTri {                  // triangle.go: v0, edge1 = v1-v0, edge2 = v2-v0
   float v0[3], e1[3], e2[3];
 };
@@ -141,11 +148,25 @@ struct alignas(16) DMaterial {
 };
 
 struct alignas(16) DTexture {
-  int32_t kind;              // 1 solid, 2 checker (even/odd solid)
-  float inv_scale;
-  int32_t pad0, pad1;
+  int32_t kind;              // 1 solid, 2 checker (even/odd solid), 3 noise, 4 image
+  float inv_scale;           // checker
+  int32_t table;             // noise: perlin index; image: image index
+  float scale;               // noise: NoiseTexture.scale
   float even[4];             // solid colour / checker even colour
   float odd[4];
+};
+
+// Perlin generator tables (noise.go:8-13).
+struct alignas(16) DPerlin {
+  float randvec[256][4];     // xyz (w unused)
+  int32_t perm[3][256];      // permX, permY, permZ
+};
+
+// ImageTexture image (image_loader.go:17-24): texels in DScene.image_texels.
+struct alignas(16) DImage {
+  int32_t width, height;
+  uint32_t offset;           // first texel
+  int32_t pad;
 };
 
 struct alignas(16) DLight {    // camera.go:610-678 (only *Quad lights contribute)
@@ -186,6 +207,10 @@ struct DScene {
   const DQuad* quads;
   const DTri* tris;
   const DTriAux* tri_aux;
+  const DCircle* circles;
+  const DPerlin* perlins;
+  const DImage* images;
+  const float* image_texels;   // 4 floats per texel: rgb (w unused), all images back to back
   const DPlane* planes;
   const DInstance* instances;
   const DBvh* blas;
@@ -197,11 +222,13 @@ struct DScene {
   const int32_t* sphere_rank;
   const int32_t* quad_rank;
   const int32_t* tri_rank;
+  const int32_t* circle_rank;
   // hit -> hittable index maps (parity probe)
   const int32_t* tlas_ref_top;   // per TLAS ref: top-level hittable index
   const int32_t* sphere_hidx;
   const int32_t* quad_hidx;
   const int32_t* tri_hidx;
+  const int32_t* circle_hidx;
   const int32_t* plane_hidx;
   const int32_t* volume_hidx;
   DBvh tlas;
@@ -213,8 +240,9 @@ struct DScene {
   int32_t stack_needed;
   int32_t has_volumes;
   int32_t has_fancy;      // a Metal / Dielectric / Isotropic material exists
+  int32_t needs_uv;       // an ImageTexture exists: hit records carry U/V
   // array lengths (bounds checks of the RTG_GUARD diagnostic build)
-  uint32_t n_nodes, n_leaves, n_refs, n_spheres, n_quads, n_tris, n_instances, n_blas, n_volumes;
+  uint32_t n_nodes, n_leaves, n_refs, n_spheres, n_quads, n_tris, n_instances, n_blas, n_volumes, n_circles;
 };
 
 struct DCamera {

@@ -193,6 +193,20 @@ __device__ __forceinline__ bool tri_t(const DTri& tr, V3 o, V3 d, float tmin, fl
   return true;
 }
 
+// Circle.Hit circle.go:37-53: plane of the disk, closed interval
+// (Contains), |P - center| <= radius.
+__device__ __forceinline__ bool circle_t(const DCircle& c, V3 o, V3 d, float tmin, float& t) {
+  V3 n = mk(c.nx, c.ny, c.nz);
+  float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return false;
+  float tt = (c.D - dot(n, o)) / denom;
+  if (!(tmin <= tt)) return false;        // upper bound checked by the caller
+  V3 p = add(o, scale(d, tt));
+  if (len(sub(p, mk(c.cx, c.cy, c.cz))) > c.r) return false;
+  t = tt;
+  return true;
+}
+
 // Plane.Hit plane.go:24-42, open interval.
 __device__ __forceinline__ bool plane_t(const DPlane& p, V3 o, V3 d, float tmin, float& t) {
   V3 n = mk(p.nx, p.ny, p.nz);
@@ -289,7 +303,7 @@ struct Best {
   int primpos;   // position inside the instance BLAS (rank), 0 otherwise
 };
 
-__device__ __forceinline__ bool closed_kind(int k) { return k == PK_QUAD || k == PK_TRI || k == PK_VOLUME; }
+__device__ __forceinline__ bool closed_kind(int k) { return k == PK_QUAD || k == PK_TRI || k == PK_VOLUME || k == PK_CIRCLE; }
 
 __device__ __forceinline__ int obj_rank(const DScene& sc, int refpos) {
   return refpos >= 0 ? sc.ref_rank[GIX(refpos, sc.n_refs, 27)] : sc.planes[GIX(-1 - refpos, sc.num_planes, 28)].rank;
@@ -301,7 +315,8 @@ __device__ __forceinline__ int prim_rank(const DScene& sc, int kind, int primpos
   const int pos = primpos & 0x3FFFFFFF;
   if (primpos < 0) return sc.ref_rank[GIX(pos, sc.n_refs, 29)];
   return kind == PK_TRI ? sc.tri_rank[GIX(pos, sc.n_tris, 30)]
-         : kind == PK_QUAD ? sc.quad_rank[GIX(pos, sc.n_quads, 31)] : sc.sphere_rank[GIX(pos, sc.n_spheres, 32)];
+         : kind == PK_QUAD ? sc.quad_rank[GIX(pos, sc.n_quads, 31)]
+         : kind == PK_CIRCLE ? sc.circle_rank[GIX(pos, sc.n_circles, 33)] : sc.sphere_rank[GIX(pos, sc.n_spheres, 32)];
 }
 // Is candidate (kind, refpos, primpos) preferred over the best at equal t?
 // Rare (exact float ties), scalar arguments only.
@@ -589,6 +604,9 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         } else if (pk == PK_SPHERE) {
           if (kCount) cnt.sph++;
           ok = sphere_t(sc.spheres[GIX(pi, sc.n_spheres, 14)], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+        } else if (kVol && pk == PK_CIRCLE) {   // kVol: the rare-primitive variant (volumes, circles)
+          if (kCount) cnt.quad++;   // counted with the quads (same kind of test)
+          ok = circle_t(sc.circles[GIX(pi, sc.n_circles, 34)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
         } else if (pk == PK_INSTANCE) {
           // world-space cull on the instance's own (padded) bbox before
           // paying for the instance fetch + object-space root test
@@ -665,6 +683,7 @@ struct Rec {
   V3 P, N;
   bool front;
   int mat;
+  float u, v;   // HitRecord.U/V (textures); 0 for planes and volumes (their Hit leaves them unset)
 };
 
 __device__ __forceinline__ void set_face(V3 d, V3 outward, Rec& rec) {
@@ -674,6 +693,8 @@ __device__ __forceinline__ void set_face(V3 d, V3 outward, Rec& rec) {
 
 __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float time) {
   Rec rec;
+  rec.u = 0.0f;
+  rec.v = 0.0f;
   if (b.kind == PK_PLANE) {
     const DPlane& p = sc.planes[b.idx];
     rec.P = add(wo, scale(wd, b.t));
@@ -693,19 +714,55 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
   const DInstance* in = nullptr;
   if (b.inst >= 0) { in = &sc.instances[GIX(b.inst, sc.n_instances, 21)]; to_object(*in, o, d); }
   rec.P = add(o, scale(d, b.t));
+  // UVs (HitRecord.U/V) only when an ImageTexture needs them
+  const bool uv = sc.needs_uv != 0;
   if (b.kind == PK_SPHERE) {
     const DSphere& s = sc.spheres[GIX(b.idx, sc.n_spheres, 22)];
     V3 c = add(mk(s.cx, s.cy, s.cz), scale(mk(s.vx, s.vy, s.vz), time));
-    set_face(d, divs(sub(rec.P, c), s.r), rec);
+    const V3 outward = divs(sub(rec.P, c), s.r);
+    set_face(d, outward, rec);
     rec.mat = s.mat;
+    if (uv) {                                     // getSphereUV sphere.go:53-59
+      const float theta = acosf(-outward.y);
+      const float phi = atan2f(-outward.z, outward.x) + kPi;
+      rec.u = phi / (2.0f * kPi);
+      rec.v = theta / kPi;
+    }
   } else if (b.kind == PK_QUAD) {
     const DQuad& q = sc.quads[GIX(b.idx, sc.n_quads, 23)];
     set_face(d, mk(q.nx, q.ny, q.nz), rec);
     rec.mat = q.mat;
+    if (uv) {                                     // quad.go:70-82: (alpha, beta)
+      const V3 ph = sub(rec.P, mk(q.Qx, q.Qy, q.Qz));
+      const V3 w = mk(q.wx, q.wy, q.wz);
+      rec.u = dot(w, cross(ph, mk(q.vx, q.vy, q.vz)));
+      rec.v = dot(w, cross(mk(q.ux, q.uy, q.uz), ph));
+    }
+  } else if (b.kind == PK_CIRCLE) {
+    const DCircle& ci = sc.circles[GIX(b.idx, sc.n_circles, 35)];
+    const V3 n = mk(ci.nx, ci.ny, ci.nz);
+    set_face(d, n, rec);
+    rec.mat = ci.mat;
+    if (uv) {                                     // circle.go:59-71
+      const V3 bu = unit(cross(fabsf(n.y) > 0.9f ? mk(1.0f, 0.0f, 0.0f) : mk(0.0f, 1.0f, 0.0f), n));
+      const V3 bv = cross(n, bu);
+      const V3 lp = sub(rec.P, mk(ci.cx, ci.cy, ci.cz));
+      rec.u = (dot(lp, bu) / ci.r + 1.0f) * 0.5f;
+      rec.v = (dot(lp, bv) / ci.r + 1.0f) * 0.5f;
+    }
   } else {  // PK_TRI
     const DTriAux& ax = sc.tri_aux[GIX(b.idx, sc.n_tris, 24)];
     set_face(d, mk(ax.nx, ax.ny, ax.nz), rec);
     rec.mat = ax.mat;
+    if (uv) {                                     // triangle.go:57-101: Moller-Trumbore (u, v)
+      const DTri& tr = sc.tris[GIX(b.idx, sc.n_tris, 36)];
+      const V3 e1 = ld3(tr.e1), e2 = ld3(tr.e2);
+      const V3 h = cross(d, e2);
+      const float f = 1.0f / dot(e1, h);
+      const V3 sv = sub(o, ld3(tr.v0));
+      rec.u = f * dot(sv, h);
+      rec.v = f * dot(d, cross(sv, e1));
+    }
   }
   if (in) {
     for (int i = in->nwrap - 1; i >= 0; --i) unwrap_hit(in->kind[i], in->prm[i], rec.P, rec.N);
@@ -716,8 +773,51 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
 // ----------------------------------------------------------------------------
 // Textures / materials
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ V3 tex_value(const DScene& sc, int ti, V3 p) {
+// Perlin.Noise / Turb (noise.go:31-67, 84-100) in fp32 on the caller's tables.
+__device__ float perlin_noise(const DPerlin& P, V3 pt) {
+  const float fx = floorf(pt.x), fy = floorf(pt.y), fz = floorf(pt.z);
+  const float u = pt.x - fx, v = pt.y - fy, w = pt.z - fz;
+  const int i = int(fx), j = int(fy), k = int(fz);
+  float accum = 0.0f;
+  for (int di = 0; di < 2; ++di)
+    for (int dj = 0; dj < 2; ++dj)
+      for (int dk = 0; dk < 2; ++dk) {
+        const int idx = P.perm[0][(i + di) & 255] ^ P.perm[1][(j + dj) & 255] ^ P.perm[2][(k + dk) & 255];
+        const V3 c = mk(P.randvec[idx][0], P.randvec[idx][1], P.randvec[idx][2]);
+        const V3 wv = mk(u - float(di), v - float(dj), w - float(dk));
+        accum += (di ? u : 1.0f - u) * (dj ? v : 1.0f - v) * (dk ? w : 1.0f - w) * dot(c, wv);
+      }
+  return accum;
+}
+__device__ float perlin_turb(const DPerlin& P, V3 pt, int depth) {
+  float accum = 0.0f, weight = 1.0f;
+  V3 tp = pt;
+  for (int i = 0; i < depth; ++i) {
+    accum += weight * perlin_noise(P, tp);
+    weight *= 0.5f;
+    tp = scale(tp, 2.0f);
+  }
+  return fabsf(accum);
+}
+
+__device__ __forceinline__ V3 tex_value(const DScene& sc, int ti, float tu, float tv, V3 p) {
   const DTexture& t = sc.textures[ti];
+  if (t.kind == 3) {                                   // NoiseTexture texture.go:81-85
+    const float s = t.scale * p.z + 10.0f * perlin_turb(sc.perlins[t.table], scale(p, t.scale), 7);
+    const float g = 0.5f * (1.0f + sinf(s));
+    return mk(g, g, g);
+  }
+  if (t.kind == 4) {                                   // ImageTexture image_texture.go:26-41
+    const DImage& im = sc.images[t.table];
+    if (im.height <= 0) return mk(0.0f, 1.0f, 1.0f);
+    const float cu = tu < 0.0f ? 0.0f : (tu > 1.0f ? 1.0f : tu);
+    const float cv = 1.0f - (tv < 0.0f ? 0.0f : (tv > 1.0f ? 1.0f : tv));
+    int x = int(cu * float(im.width)), y = int(cv * float(im.height));
+    x = x < 0 ? 0 : (x < im.width ? x : im.width - 1);             // PixelData clamp (image_loader.go:97-120)
+    y = y < 0 ? 0 : (y < im.height ? y : im.height - 1);
+    const float* tx = sc.image_texels + 4 * (size_t(im.offset) + size_t(y) * size_t(im.width) + size_t(x));
+    return mk(tx[0], tx[1], tx[2]);
+  }
   if (t.kind == 2) {                                   // texture.go:47-65
     const float eps = 1e-4f;
     int xi = int(floorf(t.inv_scale * p.x + eps));
@@ -846,12 +946,12 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
     V3 att, sd;
     bool use_mis = false;
     if (m.kind == 4) {                                        // DiffuseLight: no scatter
-      if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.P)));
+      if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.u, rec.v, rec.P)));
       break;
     } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
       sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
       if (near_zero(sd)) sd = rec.N;
-      att = tex_value(sc, m.tex, rec.P);
+      att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
       use_mis = sc.num_lights > 0;
     } else if (m.kind == 2) {                                 // Metal material.go:113-119
       V3 refl = reflect(rd, rec.N);
@@ -877,7 +977,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
       sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
     } else {                                                  // Isotropic material.go:266-270
       sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
-      att = tex_value(sc, m.tex, rec.P);
+      att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
     }
     if (use_mis) {                                            // camera.go:502-517
       int nl = sc.num_lights;
@@ -939,7 +1039,7 @@ __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, u
                                                   sb, key, bounce, DOM_VOL_SH_AREA, cnt, err);
             if (!blocked) {
               const DMaterial& lm = sc.materials[lt.mat];
-              V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, lp) : mk(0.0f, 0.0f, 0.0f);
+              V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
               float area = len(cross(ld3(lt.u), ld3(lt.v)));
               float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
               if (!(cl < 0.001f)) {

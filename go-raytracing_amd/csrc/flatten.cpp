@@ -96,7 +96,7 @@ struct Flattener {
   static bool is_wrapper(int k) {
     return k == RT_TRANSLATE || k == RT_ROTATE_X || k == RT_ROTATE_Y || k == RT_ROTATE_Z || k == RT_SCALE;
   }
-  static bool is_prim(int k) { return k == RT_SPHERE || k == RT_QUAD || k == RT_TRIANGLE; }
+  static bool is_prim(int k) { return k == RT_SPHERE || k == RT_QUAD || k == RT_TRIANGLE || k == RT_CIRCLE; }
 
   // -------------------------------------------------------------- prims
   int add_sphere(int g) {
@@ -145,14 +145,28 @@ struct Flattener {
     S.tri_rank.push_back(0);
     return int(S.tris.size()) - 1;
   }
+  int add_circle(int g) {   // circle.go:14-31
+    const rt_hittable& h = H(g);
+    DCircle c{};
+    c.cx = float(h.p[0]); c.cy = float(h.p[1]); c.cz = float(h.p[2]);
+    c.nx = float(h.p[3]); c.ny = float(h.p[4]); c.nz = float(h.p[5]);
+    c.r = float(h.p[6]);
+    c.D = float(h.p[7]);
+    c.mat = h.material;
+    S.circles.push_back(c);
+    S.circle_rank.push_back(0);
+    S.circle_hidx.push_back(g);
+    return int(S.circles.size()) - 1;
+  }
   int prim_kind(int k) const {
-    return k == RT_SPHERE ? PK_SPHERE : k == RT_QUAD ? PK_QUAD : k == RT_TRIANGLE ? PK_TRI : -1;
+    return k == RT_SPHERE ? PK_SPHERE : k == RT_QUAD ? PK_QUAD : k == RT_TRIANGLE ? PK_TRI : k == RT_CIRCLE ? PK_CIRCLE : -1;
   }
   int add_prim(int g) {
     switch (H(g).kind) {
       case RT_SPHERE: return add_sphere(g);
       case RT_QUAD: return add_quad(g);
       case RT_TRIANGLE: return add_tri(g);
+      case RT_CIRCLE: return add_circle(g);
     }
     return -1;
   }
@@ -161,6 +175,7 @@ struct Flattener {
     if (kind == RT_SPHERE) S.sphere_rank[i] = r;
     else if (kind == RT_QUAD) S.quad_rank[i] = r;
     else if (kind == RT_TRIANGLE) S.tri_rank[i] = r;
+    else if (kind == RT_CIRCLE) S.circle_rank[i] = r;
   }
 
   // Leaf over a list of primitive graph indices (BLAS level).  Homogeneous
@@ -525,7 +540,7 @@ struct Flattener {
   bool add_object_ref(int g, int rank) {
     const rt_hittable& h = H(g);
     uint32_t ref = 0;
-    if (h.kind == RT_SPHERE || h.kind == RT_QUAD || h.kind == RT_TRIANGLE) {
+    if (is_prim(h.kind)) {
       int i = add_prim(g);
       ref = (uint32_t(prim_kind(h.kind)) << REF_SHIFT) | uint32_t(i);
     } else if (h.kind == RT_VOLUME) {
@@ -831,11 +846,46 @@ struct Flattener {
           o.even[a] = float(d->textures[t.even].albedo[a]);
           o.odd[a] = float(d->textures[t.odd].albedo[a]);
         }
+      } else if (t.kind == RT_TEX_NOISE) {          // texture.go:81-85
+        if (t.perlin < 0 || t.perlin >= d->num_perlins || !d->perlins) { fail(RT_ERR_INVALID, "bad perlin index"); return; }
+        o.table = t.perlin;
+        o.scale = float(t.scale);
+      } else if (t.kind == RT_TEX_IMAGE) {          // image_texture.go:26-41
+        if (t.image < 0 || t.image >= d->num_images || !d->images) { fail(RT_ERR_INVALID, "bad image index"); return; }
+        o.table = t.image;
       } else {
         fail(RT_ERR_UNSUPPORTED, "unsupported texture kind");
         return;
       }
       S.textures.push_back(o);
+    }
+  }
+
+  // NoiseTexture generators and ImageTexture images (fp32 copies).
+  void texture_tables() {
+    for (int i = 0; i < d->num_perlins; ++i) {
+      const rt_perlin& p = d->perlins[i];
+      DPerlin o{};
+      for (int k = 0; k < 256; ++k) {
+        for (int a = 0; a < 3; ++a) o.randvec[k][a] = float(p.randvec[k][a]);
+        o.perm[0][k] = p.perm_x[k]; o.perm[1][k] = p.perm_y[k]; o.perm[2][k] = p.perm_z[k];
+        if ((o.perm[0][k] | o.perm[1][k] | o.perm[2][k]) & ~255) { fail(RT_ERR_INVALID, "perlin permutation out of range"); return; }
+      }
+      S.perlins.push_back(o);
+    }
+    for (int i = 0; i < d->num_images; ++i) {
+      const rt_image& im = d->images[i];
+      DImage o{};
+      o.width = im.width > 0 && im.rgb ? im.width : 0;
+      o.height = im.height > 0 && im.rgb ? im.height : 0;   // ImageLoader without data: Height() == 0
+      o.offset = uint32_t(S.image_texels.size() / 4);
+      for (size_t k = 0; k < size_t(o.width) * size_t(o.height); ++k) {
+        S.image_texels.push_back(float(im.rgb[3 * k]));
+        S.image_texels.push_back(float(im.rgb[3 * k + 1]));
+        S.image_texels.push_back(float(im.rgb[3 * k + 2]));
+        S.image_texels.push_back(0.0f);
+      }
+      S.images.push_back(o);
     }
   }
 
@@ -1011,6 +1061,8 @@ struct Flattener {
       }
     }
     materials();
+    if (status) return status;
+    texture_tables();
     if (status) return status;
     // empty leaf record at index 0
     S.leaves.push_back(DLeaf{0, make_leaf_info(0, PK_MIXED, 1)});

@@ -25,6 +25,12 @@ struct HostScene {
   std::vector<DTriAux> tri_aux;
   std::vector<int32_t> tri_hidx;
   std::vector<int32_t> tri_rank;
+  std::vector<DCircle> circles;
+  std::vector<int32_t> circle_hidx;
+  std::vector<int32_t> circle_rank;
+  std::vector<DPerlin> perlins;
+  std::vector<DImage> images;
+  std::vector<float> image_texels;   // 4 per texel
   std::vector<DPlane> planes;
   std::vector<int32_t> plane_hidx;
   std::vector<DInstance> instances;

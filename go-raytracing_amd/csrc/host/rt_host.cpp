@@ -4,6 +4,7 @@
 #include "rt_host.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -40,6 +41,42 @@ int CheckerTexture::emit(Emitter& e) const {
   e.textures.push_back(t);
   return int(e.textures.size()) - 1;
 }
+int NoiseTexture::emit(Emitter& e) const {
+  int pi;
+  if (!e.seen(noise.get(), pi)) {
+    rt_perlin p{};
+    for (int i = 0; i < 256; ++i) {
+      p.randvec[i][0] = noise->randvec[i].X; p.randvec[i][1] = noise->randvec[i].Y; p.randvec[i][2] = noise->randvec[i].Z;
+      p.perm_x[i] = noise->permX[i]; p.perm_y[i] = noise->permY[i]; p.perm_z[i] = noise->permZ[i];
+    }
+    e.perlins.push_back(p);
+    pi = int(e.perlins.size()) - 1;
+    e.memo[noise.get()] = pi;
+  }
+  rt_texture t{};
+  t.kind = RT_TEX_NOISE;
+  t.scale = scale;
+  t.perlin = pi;
+  e.textures.push_back(t);
+  return int(e.textures.size()) - 1;
+}
+int ImageTexture::emit(Emitter& e) const {
+  int ii;
+  if (!e.seen(image.get(), ii)) {
+    rt_image im{};
+    im.width = image->width;
+    im.height = image->height;
+    im.rgb = image->rgb.empty() ? nullptr : image->rgb.data();
+    e.images.push_back(im);
+    ii = int(e.images.size()) - 1;
+    e.memo[image.get()] = ii;
+  }
+  rt_texture t{};
+  t.kind = RT_TEX_IMAGE;
+  t.image = ii;
+  e.textures.push_back(t);
+  return int(e.textures.size()) - 1;
+}
 static int push_mat(Emitter& e, const rt_material& m) { e.materials.push_back(m); return int(e.materials.size()) - 1; }
 int Lambertian::emit(Emitter& e) const { rt_material m{}; m.kind = RT_LAMBERTIAN; m.texture = e.emit_texture(tex); return push_mat(e, m); }
 int Metal::emit(Emitter& e) const { rt_material m{}; m.kind = RT_METAL; m.texture = -1; put3(m.albedo, Albedo); m.fuzz = Fuzz; return push_mat(e, m); }
@@ -63,6 +100,12 @@ int Triangle::emit(Emitter& e) const {
   rt_hittable h = blank(RT_TRIANGLE, bbox);
   h.material = e.emit_material(mat);
   put3(h.p, v0); put3(h.p + 3, v1); put3(h.p + 6, v2); put3(h.p + 9, normal);
+  return e.add(h);
+}
+int Circle::emit(Emitter& e) const {
+  rt_hittable h = blank(RT_CIRCLE, bbox);
+  h.material = e.emit_material(mat);
+  put3(h.p, center); put3(h.p + 3, normal); h.p[6] = radius; h.p[7] = D;
   return e.add(h);
 }
 int Plane::emit(Emitter& e) const {
@@ -142,6 +185,10 @@ rt_scene_desc Emitter::desc() const {
   d.lights = lights.data();
   d.num_lights = int(lights.size());
   d.environment = env.rgb ? &env : nullptr;
+  d.images = images.empty() ? nullptr : images.data();
+  d.num_images = int(images.size());
+  d.perlins = perlins.empty() ? nullptr : perlins.data();
+  d.num_perlins = int(perlins.size());
   return d;
 }
 
@@ -184,6 +231,51 @@ HittablePtr NewPlane(Point3 p, Vec3 n, MaterialPtr m) {   // plane.go:12-19
   pl->Point = p; pl->Normal = n.Unit(); pl->Mat = std::move(m);
   pl->bbox = AABB::FromIntervals(Interval::Universe(), Interval::Universe(), Interval::Universe());
   return pl;
+}
+
+HittablePtr NewCircle(Point3 c, Vec3 n, double r, MaterialPtr m) {   // circle.go:14-31
+  auto ci = std::make_shared<Circle>();
+  ci->normal = n.Unit(); ci->center = c; ci->radius = r; ci->mat = std::move(m);
+  ci->D = Dot(ci->normal, c);
+  Vec3 rv{r, r, r};
+  ci->bbox = AABB::FromPoints(c.Sub(rv), c.Add(rv));
+  return ci;
+}
+
+std::shared_ptr<Perlin> NewPerlin(SceneRng& R) {   // noise.go:15-29, 70-82
+  auto p = std::make_shared<Perlin>();
+  for (int i = 0; i < 256; ++i) {
+    Vec3 v{R.Range(-1, 1), R.Range(-1, 1), R.Range(-1, 1)};   // RandomVec3Range(-1, 1)
+    p->randvec[i] = v.Unit();
+  }
+  for (int* perm : {p->permX, p->permY, p->permZ}) {
+    for (int i = 0; i < 256; ++i) perm[i] = i;
+    for (int i = 255; i > 0; --i) {                            // permute: RandomInt(0, i)
+      const int target = std::min(i, int(R.RandomDouble() * double(i + 1)));
+      std::swap(perm[i], perm[target]);
+    }
+  }
+  return p;
+}
+
+bool LoadPPM(const std::string& path, ImageData& img, std::string& err) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) { err = "image not found: " + path; return false; }
+  std::string magic;
+  int w = 0, h = 0, maxv = 0;
+  f >> magic >> w >> h >> maxv;
+  f.get();
+  if (magic != "P6" || w <= 0 || h <= 0 || maxv != 255) { err = "not an 8-bit binary PPM: " + path; return false; }
+  std::vector<unsigned char> px(size_t(w) * h * 3);
+  if (!f.read(reinterpret_cast<char*>(px.data()), std::streamsize(px.size()))) { err = "truncated PPM: " + path; return false; }
+  img.width = w;
+  img.height = h;
+  img.rgb.resize(px.size());
+  for (size_t i = 0; i < px.size(); ++i) {
+    const double lin = double(px[i]) / 255.0;           // RGBA() 16-bit / 65535 of an 8-bit channel
+    img.rgb[i] = lin > 0 ? std::sqrt(lin) : 0.0;        // LinearToGamma (utils.go:85-90)
+  }
+  return true;
 }
 
 HittablePtr NewTranslate(HittablePtr o, Vec3 off) {   // transform.go:84-91
@@ -260,6 +352,17 @@ HittablePtr Box(Point3 a, Point3 b, MaterialPtr m) {   // primitives.go:5-37
   sides->Add(NewQuad({mn.X, mn.Y, mn.Z}, dz, dy, m));
   sides->Add(NewQuad({mn.X, mx.Y, mx.Z}, dx, dz.Neg(), m));
   sides->Add(NewQuad({mn.X, mn.Y, mn.Z}, dx, dz, m));
+  return sides;
+}
+
+HittablePtr Pyramid(Point3 bc, double base, double height, MaterialPtr m) {   // primitives.go:39-80
+  auto sides = NewHittableList();
+  sides->Add(NewQuad({bc.X - base / 2, bc.Y, bc.Z - base / 2}, {base, 0, 0}, {0, 0, base}, m));
+  const Point3 apex{bc.X, bc.Y + height, bc.Z};
+  const double hs = base / 2;
+  const Point3 corners[4] = {{bc.X + hs, bc.Y, bc.Z - hs}, {bc.X + hs, bc.Y, bc.Z + hs},
+                             {bc.X - hs, bc.Y, bc.Z + hs}, {bc.X - hs, bc.Y, bc.Z - hs}};
+  for (int i = 0; i < 4; ++i) sides->Add(NewTriangle(corners[i], corners[(i + 1) % 4], apex, m));
   return sides;
 }
 
@@ -723,6 +826,76 @@ static bool hdri_scene(const SceneOptions& o, Scene& s, std::string& err, bool w
   return true;
 }
 
+static Scene quads_scene() {   // scenes.go:274-313
+  Scene s;
+  s.world = NewHittableList();
+  auto leftRed = NewLambertian({1.0, 0.2, 0.2});
+  auto backGreen = NewLambertian({0.2, 1.0, 0.2});
+  auto rightBlue = NewLambertian({0.2, 0.2, 1.0});
+  auto upperOrange = NewLambertian({1.0, 0.5, 0.0});
+  auto lowerTeal = NewLambertian({0.2, 0.8, 0.8});
+  s.world->Add(NewQuad({-3, -2, 5}, {0, 0, -4}, {0, 4, 0}, leftRed));
+  s.world->Add(NewQuad({-2, -2, 0}, {4, 0, 0}, {0, 4, 0}, backGreen));
+  s.world->Add(NewQuad({3, -2, 1}, {0, 0, 4}, {0, 4, 0}, rightBlue));
+  s.world->Add(NewQuad({-2, 3, 1}, {4, 0, 0}, {0, 0, 4}, upperOrange));
+  s.world->Add(NewQuad({-2, -3, 5}, {4, 0, 0}, {0, 0, -4}, lowerTeal));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(400, 1.0).SetQuality(100, 50).SetPosition({0, 0, 9}, {0, 0, 0}, {0, 1, 0})
+      .SetLens(80, 0, 10).EnableSkyGradient(true).Build();
+  return s;
+}
+
+static Scene primitives_scene() {   // scenes.go:315-410
+  Scene s;
+  s.world = NewHittableList();
+  auto redMat = NewLambertian({0.8, 0.1, 0.1});
+  auto greenMat = NewLambertian({0.1, 0.8, 0.1});
+  auto blueMat = NewLambertian({0.1, 0.1, 0.8});
+  auto metalMat = NewMetal({1.0, 1.0, 1.0}, 0);
+  auto lightMat = NewDiffuseLight(NewSolidColor({2, 2, 2}));
+  auto checkerMat = NewLambertianTexture(NewCheckerTextureFromColors(1.0, {0.0, 0.0, 0.0}, {0.9, 0.9, 0.9}));
+  s.world->Add(NewPlane({0, -1, 0}, {0, 1, 0}, checkerMat));
+  s.world->Add(NewCircle({-5, 0, 0}, {0, 1, 0}, 0.9, redMat));
+  s.world->Add(Pyramid({-2.5, -1, 0}, 1.4, 1.8, greenMat));
+  s.world->Add(NewSphere({0, 0.6, 0}, 0.8, NewDielectric(1.5)));
+  const double cubeX = 2.5, cubeSize = 1.0;
+  s.world->Add(Box({cubeX - cubeSize / 2, -1, -cubeSize / 2}, {cubeX + cubeSize / 2, -1 + cubeSize, cubeSize / 2}, blueMat));
+  auto areaLight = NewQuad({-2, 5, -2}, {4, 0, 0}, {0, 0, 4}, lightMat);
+  s.world->Add(areaLight);
+  s.world->Add(NewSphere({5, 0.6, 0}, 0.8, metalMat));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(800, 16.0 / 9.0).SetQuality(300, 25).SetPosition({0, 2, 10}, {0, 0, 0}, {0, 1, 0})
+      .SetLens(45, 0, 10).SetBackground({0, 0, 0}).EnableSkyGradient(true).AddLight(areaLight).Build();
+  return s;
+}
+
+static Scene perlin_scene(uint64_t seed) {   // scenes.go:244-270 (PerlinSpheresScene)
+  SceneRng R(seed);
+  Scene s;
+  s.world = NewHittableList();
+  auto pertext = std::make_shared<NoiseTexture>(NewPerlin(R), 4.0);
+  auto perlMaterial = NewLambertianTexture(pertext);
+  s.world->Add(NewSphere({0, 2, 0}, 2, perlMaterial));
+  s.world->Add(NewPlane({0, 0, -1}, {0, 1, 0}, perlMaterial));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(600, 16.0 / 9.0).SetQuality(100, 50).SetPosition({13, 2, -10}, {0, 1.5, 0}, {0, 1, 0})
+      .SetLens(20, 0, 10).EnableSkyGradient(true).Build();
+  return s;
+}
+
+static bool earth_scene(const SceneOptions& o, Scene& s, std::string& err) {   // scenes.go:210-242
+  auto img = std::make_shared<ImageData>();
+  const std::string dir = o.asset_dir.empty() ? std::string("assets") : o.asset_dir;
+  if (!LoadPPM(dir + "/images/earthmap.ppm", *img, err)) return false;
+  s.world = NewHittableList();
+  auto earthSurface = NewLambertianTexture(std::make_shared<ImageTexture>(img));
+  s.world->Add(NewSphere({0, 0, 0}, 2, earthSurface));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(800, 16.0 / 9.0).SetQuality(100, 50).SetPosition({0, 0, 12}, {0, 0, 0}, {0, 1, 0})
+      .SetLens(20, 0, 10).EnableSkyGradient(true).Build();
+  return true;
+}
+
 bool MakeScene(const std::string& name, const SceneOptions& opt, Scene& out, std::string& err) {
   out = Scene{};
   out.name = name;
@@ -733,6 +906,10 @@ bool MakeScene(const std::string& name, const SceneOptions& opt, Scene& out, std
   else if (name == "cornell-lucy") { if (!cornell_lucy(opt, out, err)) return false; }
   else if (name == "hdri-test") { if (!hdri_scene(opt, out, err, false)) return false; }
   else if (name == "hdri-nee") { if (!hdri_scene(opt, out, err, true)) return false; }
+  else if (name == "quads") out = quads_scene();
+  else if (name == "primitives") out = primitives_scene();
+  else if (name == "perlin") out = perlin_scene(opt.seed);
+  else if (name == "earth") { if (!earth_scene(opt, out, err)) return false; }
   else { err = "unknown scene: " + name; return false; }
   out.name = name;
   apply_overrides(*out.camera, opt);

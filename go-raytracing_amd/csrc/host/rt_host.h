@@ -114,6 +114,33 @@ struct CheckerTexture : Texture {
   CheckerTexture(double scale, TexturePtr e, TexturePtr o) : invScale(1.0 / scale), even(std::move(e)), odd(std::move(o)) {}
   int emit(Emitter& e) const override;
 };
+struct SceneRng;
+// Perlin (noise.go:8-29): tables drawn from the scene RNG (the Go code draws
+// them from the global math/rand).
+struct Perlin {
+  Vec3 randvec[256];
+  int permX[256], permY[256], permZ[256];
+};
+std::shared_ptr<Perlin> NewPerlin(SceneRng& rng);
+struct NoiseTexture : Texture {   // texture.go:19-28, 81-85
+  std::shared_ptr<Perlin> noise;
+  double scale;
+  NoiseTexture(std::shared_ptr<Perlin> p, double s) : noise(std::move(p)), scale(s) {}
+  int emit(Emitter& e) const override;
+};
+// ImageLoader data (image_loader.go:17-24): rgb after LinearToGamma.
+struct ImageData {
+  int width = 0, height = 0;
+  std::vector<double> rgb;
+};
+struct ImageTexture : Texture {   // image_texture.go:5-41
+  std::shared_ptr<ImageData> image;
+  explicit ImageTexture(std::shared_ptr<ImageData> i) : image(std::move(i)) {}
+  int emit(Emitter& e) const override;
+};
+// image_loader.go:45-80 for an 8-bit binary PPM (P6): channel v -> LinearToGamma(v/255)
+// (Go: RGBA() 16-bit / 65535 of an 8-bit image).
+bool LoadPPM(const std::string& path, ImageData& img, std::string& err);
 inline TexturePtr NewSolidColor(Color c) { return std::make_shared<SolidColor>(c); }
 inline TexturePtr NewCheckerTextureFromColors(double scale, Color a, Color b) {
   return std::make_shared<CheckerTexture>(scale, NewSolidColor(a), NewSolidColor(b));
@@ -173,6 +200,13 @@ struct Plane : Hittable {    // plane.go
 };
 HittablePtr NewPlane(Point3 p, Vec3 n, MaterialPtr m);
 
+struct Circle : Hittable {   // circle.go
+  Point3 center; Vec3 normal; double radius, D; MaterialPtr mat; AABB bbox;
+  AABB BoundingBox() const override { return bbox; }
+  int emit(Emitter& e) const override;
+};
+HittablePtr NewCircle(Point3 c, Vec3 n, double r, MaterialPtr m);
+
 struct HittableList : Hittable {
   std::vector<HittablePtr> Objects;
   AABB bbox{Interval(), Interval(), Interval()};
@@ -227,6 +261,7 @@ struct Volume : Hittable {   // volume.go
 HittablePtr NewVolumeFromColor(HittablePtr boundary, double density, Color albedo);
 
 HittablePtr Box(Point3 a, Point3 b, MaterialPtr m);   // primitives.go:5-37
+HittablePtr Pyramid(Point3 baseCenter, double baseSize, double height, MaterialPtr m);   // primitives.go:39-80
 
 // ------------------------------------------------------------------ HDRI
 struct HDRIEnvironment {     // hdri.go:13-26 (distribution built on upload)
@@ -318,6 +353,8 @@ class Emitter {
   std::vector<rt_material> materials;
   std::vector<rt_texture> textures;
   std::vector<int32_t> lights;
+  std::vector<rt_image> images;
+  std::vector<rt_perlin> perlins;
   rt_environment env{};
   std::vector<double> env_rgb;
   std::map<const void*, int> memo;

@@ -153,6 +153,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, ui
       if (b.kind == PK_SPHERE) prim = sc.sphere_hidx[b.idx];
       else if (b.kind == PK_QUAD) prim = sc.quad_hidx[b.idx];
       else if (b.kind == PK_TRI) prim = sc.tri_hidx[b.idx];
+      else if (b.kind == PK_CIRCLE) prim = sc.circle_hidx[b.idx];
       else prim = sc.volume_hidx[b.idx];
     }
   }

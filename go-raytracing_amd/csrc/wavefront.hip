@@ -325,12 +325,12 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
         V3 att = mk(0.0f, 0.0f, 0.0f);
         bool scat = true, use_mis = false;
         if (m.kind == 4) {                                        // DiffuseLight
-          if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.P)));
+          if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.u, rec.v, rec.P)));
           scat = false;
         } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
           sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
           if (near_zero(sd)) sd = rec.N;
-          att = tex_value(sc, m.tex, rec.P);
+          att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
           use_mis = sc.num_lights > 0;
         } else if (!kFancy) {
           scat = false;                                           // unreachable: no such material
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
           sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
         } else {                                                  // Isotropic material.go:266-270
           sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
-          att = tex_value(sc, m.tex, rec.P);
+          att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
         }
         if (scat) {
           if (use_mis) {                                          // camera.go:502-517 (set-up)
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
                 float cth = dot(rec.N, ldir);
                 if (cth > 0.0f) {
                   const DMaterial& lm = sc.materials[lt.mat];
-                  V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, lp) : mk(0.0f, 0.0f, 0.0f);
+                  V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
                   float area = len(cross(ld3(lt.u), ld3(lt.v)));
                   float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
                   if (!(cl < 0.001f)) {
@@ -682,7 +682,8 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
   hipError_t e;
   if ((e = hipMemsetAsync(a.acc, 0, size_t(a.npix) * 3 * sizeof(double), st)) != hipSuccess) return e;
   if (plan.max_depth > 0) {
-    const bool vol = sc.has_volumes != 0;
+    // the kVol variants also carry the rare primitives (circles)
+    const bool vol = sc.has_volumes != 0 || sc.n_circles > 0;
 #define RUN(S, C, V)                                                              \
   do {                                                                            \
     if (envis) {                                                                  \

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -68,8 +68,10 @@ enum rt_hittable_kind {
   RT_ROTATE_Y = 10,   /* transform.go:113-118 a=Obj p[0]=SinTheta p[1]=CosTheta */
   RT_ROTATE_Z = 11,   /* transform.go:275-280 a=Obj p[0]=SinTheta p[1]=CosTheta */
   RT_SCALE = 12,      /* transform.go:360-365 a=Obj p[0..2]=Factor p[3..5]=InvFactor */
-  RT_VOLUME = 13      /* volume.go:9-13   a=boundary p[0]=negInvDensity
+  RT_VOLUME = 13,     /* volume.go:9-13   a=boundary p[0]=negInvDensity
                                           material=phaseFunction (Isotropic)   */
+  RT_CIRCLE = 14      /* circle.go:5-12   p[0..2]=center p[3..5]=normal (unit)
+                                          p[6]=radius p[7]=D                   */
 };
 
 typedef struct rt_hittable {
@@ -99,8 +101,10 @@ typedef struct rt_material {
 } rt_material;
 
 enum rt_texture_kind {
-  RT_TEX_SOLID = 1,  /* SolidColor, texture.go:9-11,43-45                    */
-  RT_TEX_CHECKER = 2 /* CheckerTexture, texture.go:13-17,47-77               */
+  RT_TEX_SOLID = 1,   /* SolidColor, texture.go:9-11,43-45                   */
+  RT_TEX_CHECKER = 2, /* CheckerTexture, texture.go:13-17,47-77              */
+  RT_TEX_NOISE = 3,   /* NoiseTexture, texture.go:19-28,81-85 (Perlin turb)  */
+  RT_TEX_IMAGE = 4    /* ImageTexture, image_texture.go:5-41                 */
 };
 
 typedef struct rt_texture {
@@ -108,7 +112,24 @@ typedef struct rt_texture {
   int32_t even, odd; /* checker: texture indices (must be RT_TEX_SOLID)      */
   double albedo[3];  /* solid colour                                         */
   double inv_scale;  /* checker invScale                                     */
+  double scale;      /* noise: NoiseTexture.scale                            */
+  int32_t perlin;    /* noise: index into rt_scene_desc.perlins              */
+  int32_t image;     /* image: index into rt_scene_desc.images               */
 } rt_texture;
+
+/* ImageLoader (image_loader.go:17-24) as the Go loader leaves it: linear
+ * float64 rgb after LinearToGamma (image_loader.go:70-76), row-major.       */
+typedef struct rt_image {
+  int32_t width, height;
+  const double* rgb;       /* width*height*3                                */
+} rt_image;
+
+/* Perlin (noise.go:8-13): the generator's tables (NewPerlin draws them from
+ * math/rand, so the caller passes them).                                   */
+typedef struct rt_perlin {
+  double randvec[256][3];
+  int32_t perm_x[256], perm_y[256], perm_z[256];
+} rt_perlin;
 
 /* ---- HDRI environment (hdri.go:13-26, image_loader.go:17-24) ------------- */
 typedef struct rt_environment {
@@ -131,6 +152,10 @@ typedef struct rt_scene_desc {
   const int32_t* lights;     /* Camera.Lights (camera.go:38), hittable indices */
   int32_t num_lights;
   const rt_environment* environment; /* Camera.Environment or NULL (camera.go:39) */
+  const rt_image* images;    /* ImageTexture images                          */
+  int32_t num_images;
+  const rt_perlin* perlins;  /* NoiseTexture generators                      */
+  int32_t num_perlins;
 } rt_scene_desc;
 
 /* ---- camera: the state Camera.Initialize() leaves (camera.go:286-344) ---- */

@@ -154,6 +154,7 @@ static void oscene_free(OScene* os) {
 #define SIN sin
 #define ATAN2 atan2
 #define ASIN asin
+#define ACOS acos
 #define FLOOR floor
 #define POW5(x) pow((x), 5.0)
 #define PI_R M_PI
@@ -170,6 +171,7 @@ static void oscene_free(OScene* os) {
 #undef SIN
 #undef ATAN2
 #undef ASIN
+#undef ACOS
 #undef FLOOR
 #undef POW5
 #undef PI_R
@@ -198,6 +200,7 @@ static inline float o_round_up(double x) {
 #define SIN sinf
 #define ATAN2 atan2f
 #define ASIN asinf
+#define ACOS acosf
 #define FLOOR floorf
 #define POW5(x) o_pow5f(x)
 #define PI_R 3.14159265358979323846f

@@ -138,6 +138,7 @@ typedef struct {
   REAL t;
   int front;
   int top, prim;
+  REAL u, v;                     /* HitRecord.U/V (kept from earlier hits where a Hit leaves them) */
 } FN(Rec);
 
 typedef struct { V3R o, d; REAL tm; } FN(Ray);
@@ -184,7 +185,10 @@ static int FN(sphere_hit)(FN(TC)* c, int g, FN(Ray) r, REAL mn, REAL mx, FN(Rec)
   }
   rec->t = root;
   rec->P = FN(at)(r, root);
-  FN(set_face)(rec, r, FN(divs)(FN(sub)(rec->P, center), p[6]));
+  V3R outward = FN(divs)(FN(sub)(rec->P, center), p[6]);
+  FN(set_face)(rec, r, outward);
+  rec->u = (ATAN2(-outward.z, outward.x) + PI_R) / (2 * PI_R);   /* getSphereUV sphere.go:53-59 */
+  rec->v = ACOS(-outward.y) / PI_R;
   rec->mat = c->S->os->d->hittables[g].material;
   rec->prim = g;
   return 1;
@@ -206,6 +210,8 @@ static int FN(quad_hit)(FN(TC)* c, int g, FN(Ray) r, REAL mn, REAL mx, FN(Rec)* 
   if (!(0 <= alpha && alpha <= 1) || !(0 <= beta && beta <= 1)) return 0;
   rec->t = t;
   rec->P = P;
+  rec->u = alpha;                                                /* quad.go:81-82 */
+  rec->v = beta;
   rec->mat = c->S->os->d->hittables[g].material;
   FN(set_face)(rec, r, n);
   rec->prim = g;
@@ -232,8 +238,34 @@ static int FN(tri_hit)(FN(TC)* c, int g, FN(Ray) r, REAL mn, REAL mx, FN(Rec)* r
   if (!(mn <= t && t <= mx)) return 0;
   rec->t = t;
   rec->P = FN(at)(r, t);
+  rec->u = u;                                                    /* triangle.go:100-101 */
+  rec->v = v;
   rec->mat = c->S->os->d->hittables[g].material;
   FN(set_face)(rec, r, FN(mk)(p[9], p[10], p[11]));
+  rec->prim = g;
+  return 1;
+}
+
+/* Circle.Hit circle.go:37-72 */
+static int FN(circle_hit)(FN(TC)* c, int g, FN(Ray) r, REAL mn, REAL mx, FN(Rec)* rec) {
+  const REAL* p = c->S->h[g].p;
+  V3R n = FN(mk)(p[3], p[4], p[5]);
+  REAL denom = FN(dot)(n, r.d);
+  if (FABS(denom) < (REAL)1e-8) return 0;
+  REAL t = (p[7] - FN(dot)(n, r.o)) / denom;
+  if (!(mn <= t && t <= mx)) return 0;
+  V3R P = FN(at)(r, t);
+  V3R ctr = FN(mk)(p[0], p[1], p[2]);
+  if (FN(len)(FN(sub)(P, ctr)) > p[6]) return 0;
+  rec->t = t;
+  rec->P = P;
+  rec->mat = c->S->os->d->hittables[g].material;
+  FN(set_face)(rec, r, n);
+  V3R bu = FN(unit)(FN(cross)(FABS(n.y) > (REAL)0.9 ? FN(mk)(1, 0, 0) : FN(mk)(0, 1, 0), n));
+  V3R bv = FN(cross)(n, bu);
+  V3R lp = FN(sub)(P, ctr);
+  rec->u = (FN(dot)(lp, bu) / p[6] + 1) * (REAL)0.5;
+  rec->v = (FN(dot)(lp, bv) / p[6] + 1) * (REAL)0.5;
   rec->prim = g;
   return 1;
 }
@@ -293,6 +325,7 @@ static int FN(hit)(FN(TC)* c, int g, FN(Ray) r, REAL mn, REAL mx, FN(Rec)* rec) 
     case RT_QUAD: ok = FN(quad_hit)(c, g, r, mn, mx, rec); break;
     case RT_TRIANGLE: ok = FN(tri_hit)(c, g, r, mn, mx, rec); break;
     case RT_PLANE: ok = FN(plane_hit)(c, g, r, mn, mx, rec); break;
+    case RT_CIRCLE: ok = FN(circle_hit)(c, g, r, mn, mx, rec); break;
     case RT_VOLUME: ok = FN(volume_hit)(c, g, r, mn, mx, rec); break;
     case RT_LIST: {                                   /* hittable_list.go:31-45 */
       FN(Rec) tmp;
@@ -386,12 +419,59 @@ static int FN(world_hit)(FN(TC)* c, uint32_t dom, FN(Ray) r, REAL mn, REAL mx, F
   if (c->S->os->nvol) memset(c->volcount, 0, sizeof(int) * (size_t)c->S->os->nvol);
   c->voldom = dom;
   rec->top = rec->prim = -1;
+  rec->u = rec->v = 0;                                   /* rec := &HitRecord{} (camera.go:449) */
   return FN(hit)(c, c->S->os->d->root, r, mn, mx, rec);
 }
 
 /* ------------------------------------------------------------ textures / HDRI */
-static V3R FN(tex_value)(const FN(OS)* S, int ti, V3R p) {                 /* texture.go:43-77 */
+/* Perlin.Noise / Turb noise.go:31-67, 84-100 */
+static REAL FN(perlin_noise)(const rt_perlin* P, V3R pt) {
+  REAL fx = FLOOR(pt.x), fy = FLOOR(pt.y), fz = FLOOR(pt.z);
+  REAL u = pt.x - fx, v = pt.y - fy, w = pt.z - fz;
+  int i = (int)fx, j = (int)fy, k = (int)fz;
+  REAL accum = 0;
+  for (int di = 0; di < 2; ++di)
+    for (int dj = 0; dj < 2; ++dj)
+      for (int dk = 0; dk < 2; ++dk) {
+        int idx = P->perm_x[(i + di) & 255] ^ P->perm_y[(j + dj) & 255] ^ P->perm_z[(k + dk) & 255];
+        V3R cv = FN(mk)((REAL)P->randvec[idx][0], (REAL)P->randvec[idx][1], (REAL)P->randvec[idx][2]);
+        V3R wv = FN(mk)(u - (REAL)di, v - (REAL)dj, w - (REAL)dk);
+        accum += ((REAL)di * u + (1 - (REAL)di) * (1 - u)) * ((REAL)dj * v + (1 - (REAL)dj) * (1 - v)) *
+                 ((REAL)dk * w + (1 - (REAL)dk) * (1 - w)) * FN(dot)(cv, wv);
+      }
+  return accum;
+}
+static REAL FN(perlin_turb)(const rt_perlin* P, V3R pt, int depth) {
+  REAL accum = 0, weight = 1;
+  V3R tp = pt;
+  for (int i = 0; i < depth; ++i) {
+    accum += weight * FN(perlin_noise)(P, tp);
+    weight *= (REAL)0.5;
+    tp = FN(scale)(tp, 2);
+  }
+  return FABS(accum);
+}
+
+static V3R FN(tex_value)(const FN(OS)* S, int ti, REAL tu, REAL tv, V3R p) {   /* texture.go:43-85 */
   const rt_texture* t = &S->os->d->textures[ti];
+  if (t->kind == RT_TEX_NOISE) {                                       /* texture.go:81-85 */
+    const rt_perlin* P = &S->os->d->perlins[t->perlin];
+    REAL sc = (REAL)t->scale;
+    REAL s = sc * p.z + 10 * FN(perlin_turb)(P, FN(scale)(p, sc), 7);
+    REAL gv = (REAL)0.5 * (1 + SIN(s));
+    return FN(mk)(gv, gv, gv);
+  }
+  if (t->kind == RT_TEX_IMAGE) {                                       /* image_texture.go:26-41 */
+    const rt_image* im = &S->os->d->images[t->image];
+    if (im->height <= 0 || !im->rgb) return FN(mk)(0, 1, 1);
+    REAL cu = tu < 0 ? 0 : (tu > 1 ? 1 : tu);
+    REAL cv = 1 - (tv < 0 ? 0 : (tv > 1 ? 1 : tv));
+    int x = (int)(cu * (REAL)im->width), y = (int)(cv * (REAL)im->height);
+    x = x < 0 ? 0 : (x < im->width ? x : im->width - 1);              /* image_loader.go:97-120 */
+    y = y < 0 ? 0 : (y < im->height ? y : im->height - 1);
+    const double* px = im->rgb + 3 * ((size_t)y * (size_t)im->width + (size_t)x);
+    return FN(mk)((REAL)px[0], (REAL)px[1], (REAL)px[2]);
+  }
   if (t->kind == RT_TEX_CHECKER) {
     const REAL eps = (REAL)1e-4;
     REAL inv = (REAL)t->inv_scale;
@@ -528,7 +608,7 @@ static V3R FN(sample_lights)(FN(TC)* c, const FN(Rec)* rec, V3R rdir, V3R att) {
         FN(Rec) srec;
         if (!FN(world_hit)(c, O_DOM_VOL_SH_AREA, sr, (REAL)0.001, dist - (REAL)0.001, &srec)) {
           const rt_material* lm = &d->materials[lh->material];
-          V3R em = lm->kind == RT_DIFFUSE_LIGHT ? FN(tex_value)(S, lm->texture, lp) : FN(mk)(0, 0, 0);
+          V3R em = lm->kind == RT_DIFFUSE_LIGHT ? FN(tex_value)(S, lm->texture, 0, 0, lp) : FN(mk)(0, 0, 0);
           REAL area = FN(len)(FN(cross)(lu, lv));
           REAL cl = FABS(FN(dot)(FN(mk)(p[12], p[13], p[14]), FN(neg)(ldir)));
           if (!(cl < (REAL)0.001)) {
@@ -567,14 +647,14 @@ static V3R FN(ray_color)(FN(TC)* c, FN(Ray) r, int depth, uint32_t bounce, int a
   }
   const rt_material* m = &os->d->materials[rec.mat];
   V3R Le = FN(mk)(0, 0, 0);
-  if (m->kind == RT_DIFFUSE_LIGHT) Le = FN(tex_value)(S, m->texture, rec.P);  /* Emitted */
+  if (m->kind == RT_DIFFUSE_LIGHT) Le = FN(tex_value)(S, m->texture, rec.u, rec.v, rec.P);  /* Emitted */
   V3R att, sd;
   int scat = 1;
   switch (m->kind) {
     case RT_LAMBERTIAN:                                                      /* material.go:57-68 */
       sd = FN(add)(rec.N, FN(random_unit_vector)(c, O_DOM_SCATTER, 0));
       if (FN(near_zero)(sd)) sd = rec.N;
-      att = FN(tex_value)(S, m->texture, rec.P);
+      att = FN(tex_value)(S, m->texture, rec.u, rec.v, rec.P);
       break;
     case RT_METAL: {                                                         /* material.go:113-119 */
       V3R refl = FN(reflect)(r.d, rec.N);
@@ -605,7 +685,7 @@ static V3R FN(ray_color)(FN(TC)* c, FN(Ray) r, int depth, uint32_t bounce, int a
     }
     case RT_ISOTROPIC:                                                       /* material.go:266-270 */
       sd = FN(random_unit_vector)(c, O_DOM_SCATTER, 0);
-      att = FN(tex_value)(S, m->texture, rec.P);
+      att = FN(tex_value)(S, m->texture, rec.u, rec.v, rec.P);
       break;
     default:                                                                 /* DiffuseLight */
       scat = 0;

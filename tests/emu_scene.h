@@ -42,7 +42,9 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   DScene& d = E.d;
   d.nodes = ptr(h.nodes4); d.leaves = ptr(h.leaves); d.refs = ptr(h.refs); d.ref_rank = ptr(h.ref_rank);
   d.ref_box = ptr(h.ref_box); d.spheres = ptr(h.spheres); d.quads = ptr(h.quads); d.tris = ptr(h.tris);
-  d.tri_aux = ptr(h.tri_aux); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
+  d.tri_aux = ptr(h.tri_aux); d.circles = ptr(h.circles); d.circle_rank = ptr(h.circle_rank);
+  d.circle_hidx = ptr(h.circle_hidx); d.perlins = ptr(h.perlins); d.images = ptr(h.images);
+  d.image_texels = ptr(h.image_texels); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
   d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
   d.tri_rank = ptr(h.tri_rank); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);
@@ -60,6 +62,10 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
   d.n_volumes = uint32_t(h.volumes.size());
+  d.n_circles = uint32_t(h.circles.size());
+  d.needs_uv = 0;
+  for (const DTexture& t : h.textures)
+    if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
   d.has_fancy = 0;
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;

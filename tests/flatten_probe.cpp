@@ -114,6 +114,7 @@ int main(int argc, char** argv) {
         case PK_SPHERE: CHECK(pi < S.spheres.size(), "sphere index"); break;
         case PK_QUAD: CHECK(pi < S.quads.size(), "quad index"); break;
         case PK_TRI: CHECK(pi < S.tris.size(), "tri index"); break;
+        case PK_CIRCLE: CHECK(pi < S.circles.size(), "circle index"); break;
         case PK_INSTANCE: CHECK(pi < S.instances.size(), "instance index"); break;
         case PK_VOLUME: CHECK(pi < S.volumes.size(), "volume index"); break;
         default: CHECK(false, "bad prim kind in leaf");

@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol(g, header, lib):
 
 
 def test_abi_version(g):
-    assert g.rtgpu().rt_abi_version() == 2
+    assert g.rtgpu().rt_abi_version() == 3
 
 
 def test_no_silent_cpu_fallback_without_gpu(g):
@@ -47,7 +47,8 @@ def test_scene_desc_struct_sizes(g):
     # layout the Go side mirrors in INTEGRATION.md
     assert C.sizeof(g.RtHittable) == 4 * 4 + 6 * 8 + 16 * 8
     assert C.sizeof(g.RtMaterial) == 8 + 5 * 8
-    assert C.sizeof(g.RtTexture) == 16 + 4 * 8
+    assert C.sizeof(g.RtTexture) == 16 + 5 * 8 + 8
+    assert C.sizeof(g.RtPerlin) == 256 * 3 * 8 + 3 * 256 * 4
 
 
 def test_ctypes_mirror_matches_c_header(g, tmp_path):
@@ -59,7 +60,8 @@ def test_ctypes_mirror_matches_c_header(g, tmp_path):
     names = {"rt_hittable": g.RtHittable, "rt_material": g.RtMaterial, "rt_texture": g.RtTexture,
              "rt_work_counts": g.RtWorkCounts, "rt_kernel_times": g.RtKernelTimes,
              "rt_scene_info": g.RtSceneInfo, "rt_camera_desc": g.RtCameraDesc,
-             "rt_render_params": g.RtRenderParams, "rt_scene_desc": g.RtSceneDesc, "rt_stats": g.RtStats}
+             "rt_render_params": g.RtRenderParams, "rt_scene_desc": g.RtSceneDesc, "rt_stats": g.RtStats,
+             "rt_image": g.RtImage, "rt_perlin": g.RtPerlin}
     src = tmp_path / "probe.c"
     inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
     body = "".join(f'  printf("{n} %zu\\n", sizeof({n}));\n' for n in names)

@@ -28,7 +28,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "go-raytracing_amd", "lib")
 CSRC = os.path.join(ROOT, "go-raytracing_amd", "csrc")
 ASSETS = os.path.join(ROOT, "assets")
-SCENES = ["simple", "random", "cornell", "cornell-smoke", "cornell-lucy", "hdri-test", "hdri-nee"]
+SCENES = ["simple", "random", "cornell", "cornell-smoke", "cornell-lucy", "hdri-test", "hdri-nee", "quads",
+          "primitives", "perlin", "earth"]
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
 
@@ -80,7 +81,8 @@ def test_flattened_indices_in_range(probe, name):
         assert info["culling_boxes"] == info["instances"] == 10   # RotateY/Translate/Scale only
 
 
-@pytest.mark.parametrize("name", ["simple", "cornell", "cornell-smoke", "cornell-lucy", "hdri-nee"])
+@pytest.mark.parametrize("name", ["simple", "cornell", "cornell-smoke", "cornell-lucy", "hdri-nee", "primitives",
+                                  "perlin", "earth"])
 def test_device_source_under_asan_matches_oracle(emu, O, g, tmp_path, name):
     spp, seed = 2, 77
     out = tmp_path / f"{name}.f32"
@@ -99,7 +101,8 @@ def test_device_source_under_asan_matches_oracle(emu, O, g, tmp_path, name):
 
 
 @pytest.mark.parametrize("name,batch", [("simple", 0), ("cornell", 1), ("cornell-smoke", 0), ("cornell-lucy", 1),
-                                        ("hdri-nee", 0), ("random", 0)])
+                                        ("hdri-nee", 0), ("random", 0), ("primitives", 1), ("perlin", 0),
+                                        ("earth", 0)])
 def test_wavefront_kernels_under_asan_match_oracle(wave, O, g, tmp_path, name, batch):
     spp, seed, width = 2, 77, 40
     out = tmp_path / f"{name}.f32"

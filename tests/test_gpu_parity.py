@@ -21,6 +21,10 @@ SCENES = [
     ("cornell-lucy", dict(width=64, **LUCY)),
     ("hdri-test", dict(width=96)),
     ("hdri-nee", dict(width=96)),
+    ("quads", dict(width=64)),
+    ("primitives", dict(width=96)),
+    ("perlin", dict(width=96)),
+    ("earth", dict(width=96)),
 ]
 
 
@@ -42,7 +46,8 @@ def test_primary_hits_bit_exact(g, O, ctx, name, kw):
         allowed = 0 if "cornell" not in name or name == "cornell-lucy" else max(1, tg.size // 2000)
         assert mism.size <= allowed, f"{name}: {mism.size} mismatches, first {mism[:5]}"
         same = (tg == to) & (pg == po) & (tg >= 0)
-        if name in ("simple", "random", "cornell-lucy", "hdri-test", "hdri-nee"):
+        if name in ("simple", "random", "cornell-lucy", "hdri-test", "hdri-nee", "quads", "primitives", "perlin",
+                    "earth"):
             assert np.array_equal(t_g[same], t_o[same].astype(np.float32)), f"{name}: hit t differs"
         assert (tg >= 0).any()
 

@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
   a.slots = uint32_t(S);
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
-  const bool vol = d.has_volumes != 0, envis = d.env.valid && d.env.use_is, fancy = d.has_fancy != 0;
+  const bool vol = d.has_volumes != 0 || d.n_circles > 0, envis = d.env.valid && d.env.use_is, fancy = d.has_fancy != 0;
 #define RUN(V, H, F) run<V, H, F>(d, cam, a, spp, spb, E.max_depth, out.data())
   if (vol) {
     if (envis) { if (fancy) RUN(true, true, true); else RUN(true, true, false); }
