@@ -87,7 +87,11 @@ class RtCameraDesc(C.Structure):
                 ("defocus_angle", C.c_double), ("defocus_disk_u", C.c_double * 3),
                 ("defocus_disk_v", C.c_double * 3), ("background", C.c_double * 3),
                 ("use_sky_gradient", C.c_int32), ("phantom_hdri", C.c_int32), ("camera_motion", C.c_int32),
-                ("free_camera", C.c_int32)]
+                ("free_camera", C.c_int32), ("center_motion_orig", C.c_double * 3),
+                ("center_motion_dir", C.c_double * 3), ("look_at_motion_orig", C.c_double * 3),
+                ("look_at_motion_dir", C.c_double * 3), ("vup", C.c_double * 3), ("forward", C.c_double * 3),
+                ("viewport_width", C.c_double), ("viewport_height", C.c_double), ("focus_dist", C.c_double),
+                ("defocus_radius", C.c_double)]
 
 
 class RtBucket(C.Structure):
@@ -126,7 +130,9 @@ class RtSceneInfo(C.Structure):
 class RtsSceneOptions(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("width", C.c_int32), ("aspect", C.c_double), ("spp", C.c_int32),
                 ("max_depth", C.c_int32), ("asset_dir", C.c_char_p), ("obj_path", C.c_char_p),
-                ("lucy_rings", C.c_int32), ("lucy_cols", C.c_int32)]
+                ("lucy_rings", C.c_int32), ("lucy_cols", C.c_int32), ("camera_motion", C.c_int32),
+                ("look_from2", C.c_double * 3), ("look_at2", C.c_double * 3), ("free_camera", C.c_int32),
+                ("forward", C.c_double * 3)]
 
 
 _rtgpu = None
@@ -235,11 +241,22 @@ class Scene:
 
     def __init__(self, name: str, *, seed: int = 0x5EED, width: int = 0, aspect: float = 0.0, spp: int = 0,
                  max_depth: int = 0, asset_dir: Optional[str] = None, obj_path: Optional[str] = None,
-                 lucy_rings: int = 0, lucy_cols: int = 0):
+                 lucy_rings: int = 0, lucy_cols: int = 0, motion: Optional[Sequence[Sequence[float]]] = None,
+                 free_forward: Optional[Sequence[float]] = None):
+        """`motion=(look_from2, look_at2)` applies Camera.SetMotion and
+        `free_forward=(x, y, z)` Camera.EnableFreeCamera(LookFrom, forward,
+        Vup) to the scene's camera before Build() (camera.go:204-232)."""
         lib = rtscene()
         self.name = name
         opt = RtsSceneOptions(seed, width, aspect, spp, max_depth, (asset_dir or ASSET_DIR).encode(),
                               obj_path.encode() if obj_path else None, lucy_rings, lucy_cols)
+        if motion is not None:
+            opt.camera_motion = 1
+            opt.look_from2[:] = [float(x) for x in motion[0]]
+            opt.look_at2[:] = [float(x) for x in motion[1]]
+        if free_forward is not None:
+            opt.free_camera = 1
+            opt.forward[:] = [float(x) for x in free_forward]
         h = C.c_void_p()
         err = C.create_string_buffer(512)
         rc = lib.rts_scene_create(name.encode(), C.byref(opt), C.byref(h), err, 512)

@@ -129,8 +129,6 @@ void free_buf(DevBuf& b) {
 int make_camera(rt_ctx* ctx, const rt_camera_desc* c, DCamera& o) {
   if (!c) return set_err(ctx, RT_ERR_INVALID, "camera is NULL");
   if (c->image_width <= 0 || c->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
-  if (c->camera_motion || c->free_camera)
-    return set_err(ctx, RT_ERR_UNSUPPORTED, "camera motion / free camera (camera.go:390-434) not supported");
   for (int a = 0; a < 3; ++a) {
     o.center[a] = float(c->center[a]);
     o.pixel00[a] = float(c->pixel00[a]);
@@ -146,6 +144,22 @@ int make_camera(rt_ctx* ctx, const rt_camera_desc* c, DCamera& o) {
   o.cam_max_depth = c->max_depth;
   o.width = c->image_width;
   o.height = c->image_height;
+  o.slow = (c->camera_motion || c->free_camera) ? 1 : 0;   // camera.go:373
+  o.free_cam = c->free_camera ? 1 : 0;
+  for (int a = 0; a < 3; ++a) {
+    o.c_orig[a] = float(c->center_motion_orig[a]);
+    o.c_dir[a] = float(c->center_motion_dir[a]);
+    o.la_orig[a] = float(c->look_at_motion_orig[a]);
+    o.la_dir[a] = float(c->look_at_motion_dir[a]);
+    o.vup[a] = float(c->vup[a]);
+    o.fwd[a] = float(c->forward[a]);
+  }
+  o.vw = float(c->viewport_width);
+  o.vh = float(c->viewport_height);
+  o.focus = float(c->focus_dist);
+  o.radius = float(c->defocus_radius);
+  if (o.slow && !(c->viewport_width > 0.0 && c->viewport_height > 0.0))
+    return set_err(ctx, RT_ERR_INVALID, "moving / free camera needs viewport_width and viewport_height");
   return RT_OK;
 }
 

@@ -256,6 +256,12 @@ struct DCamera {
   int32_t phantom;
   int32_t cam_max_depth; // Camera.MaxDepth (camera.go:456)
   int32_t width, height;
+  // GetRay slow path (camera.go:390-434): CameraMotion or FreeCamera
+  int32_t slow, free_cam;
+  float c_orig[3], c_dir[3];    // centerMotion
+  float la_orig[3], la_dir[3];  // lookAtMotion
+  float vup[3], fwd[3];
+  float vw, vh, focus, radius;
 };
 
 // RNG counter layout: counter = bounce<<16 | domain<<12 | index

@@ -895,27 +895,67 @@ __device__ float env_pdf(const DEnv& e, V3 dir) {          // hdri.go:262-297
 }
 
 // ----------------------------------------------------------------------------
+// GetRay (camera.go:368-434): jitter, rayTime, optional defocus disk.  The
+// static camera uses Initialize()'s cached pixel grid; CameraMotion /
+// FreeCamera rebuild the basis at rayTime (slow path :390-434).
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ V3 disk_point(uint32_t key) {   // RandomInUnitDisk (vec3.go:66-77)
+  V3 p = mk(0.0f, 0.0f, 0.0f);
+  for (int k = 0; k < MAX_DISK_TRIES; ++k) {
+    uint32_t c = ctr(0, DOM_CAMERA, 3u + 2u * k);
+    float x = -1.0f + 2.0f * rnd(key, c), y = -1.0f + 2.0f * rnd(key, c + 1u);
+    if (x * x + y * y + 0.0f * 0.0f < 1.0f) { p = mk(x, y, 0.0f); break; }
+  }
+  return p;
+}
+
+__device__ __noinline__ void get_ray_slow(const DCamera& cam, int px, int py, uint32_t key, float offx, float offy,
+                                          float time, V3& ro, V3& rd) {
+  V3 center = add(ld3(cam.c_orig), scale(ld3(cam.c_dir), time));          // centerMotion.At(rayTime)
+  V3 w;
+  if (cam.free_cam) w = neg(ld3(cam.fwd));
+  else w = unit(sub(center, add(ld3(cam.la_orig), scale(ld3(cam.la_dir), time))));
+  V3 u = unit(cross(ld3(cam.vup), w));
+  V3 v = cross(w, u);
+  V3 vu = scale(u, cam.vw);
+  V3 vv = scale(neg(v), cam.vh);
+  V3 du = divs(vu, float(cam.width));
+  V3 dv = divs(vv, float(cam.height));
+  V3 ul = sub(sub(sub(center, scale(w, cam.focus)), divs(vu, 2.0f)), divs(vv, 2.0f));
+  V3 p00 = add(ul, scale(add(du, dv), 0.5f));
+  V3 ps = add(add(p00, scale(du, float(px) + offx)), scale(dv, float(py) + offy));
+  ro = center;
+  if (cam.defocus) {                                                       // defocusDiskSample :354-362
+    V3 p = disk_point(key);
+    ro = add(add(center, scale(scale(u, cam.radius), p.x)), scale(scale(v, cam.radius), p.y));
+  }
+  rd = sub(ps, ro);
+}
+
+__device__ __forceinline__ void get_ray(const DCamera& cam, int px, int py, uint32_t key, V3& ro, V3& rd,
+                                        float& time) {
+  float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
+  float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
+  time = rnd(key, ctr(0, DOM_CAMERA, 2));
+  if (cam.slow) { get_ray_slow(cam, px, py, key, offx, offy, time, ro, rd); return; }
+  V3 ps = add(add(ld3(cam.pixel00), scale(ld3(cam.du), float(px) + offx)), scale(ld3(cam.dv), float(py) + offy));
+  ro = ld3(cam.center);
+  if (cam.defocus) {
+    V3 p = disk_point(key);
+    ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
+  }
+  rd = sub(ps, ro);
+}
+
+// ----------------------------------------------------------------------------
 // One camera sample (RayColor camera.go:438-518, iterative throughput form)
 // ----------------------------------------------------------------------------
 template <bool kCount>
 __device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, uint32_t key, int depth,
                          const TStack& S, Cnt& cnt, int* err) {
-  // GetRay camera.go:368-388
-  float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
-  float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
-  float time = rnd(key, ctr(0, DOM_CAMERA, 2));
-  V3 ps = add(add(ld3(cam.pixel00), scale(ld3(cam.du), float(px) + offx)), scale(ld3(cam.dv), float(py) + offy));
-  V3 ro = ld3(cam.center);
-  if (cam.defocus) {                       // defocusDiskSample camera.go:354-362
-    V3 p = mk(0.0f, 0.0f, 0.0f);
-    for (int k = 0; k < MAX_DISK_TRIES; ++k) {
-      uint32_t c = ctr(0, DOM_CAMERA, 3u + 2u * k);
-      float x = -1.0f + 2.0f * rnd(key, c), y = -1.0f + 2.0f * rnd(key, c + 1u);
-      if (x * x + y * y + 0.0f * 0.0f < 1.0f) { p = mk(x, y, 0.0f); break; }
-    }
-    ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
-  }
-  V3 rd = sub(ps, ro);
+  V3 ro, rd;
+  float time;
+  get_ray(cam, px, py, key, ro, rd, time);
 
   V3 L = mk(0.0f, 0.0f, 0.0f), beta = mk(1.0f, 1.0f, 1.0f);
   bool allow = true;

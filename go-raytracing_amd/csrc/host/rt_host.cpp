@@ -419,7 +419,11 @@ std::shared_ptr<BVHNode> NewBVHNodeFromList(const HittableList& list) {
 }
 
 // ============================================================ camera
-void Camera::Initialize() {   // camera.go:286-344 (static camera)
+void Camera::Initialize() {   // camera.go:286-344
+  centerMotionOrig = LookFrom;
+  lookAtMotionOrig = LookAt;
+  centerMotionDir = CameraMotion ? LookFrom2.Sub(LookFrom) : Vec3{0, 0, 0};
+  lookAtMotionDir = CameraMotion ? LookAt2.Sub(LookAt) : Vec3{0, 0, 0};
   ImageHeight = std::max(int(double(ImageWidth) / AspectRatio), 1);
   pixelsSamplesScale = 1.0 / double(SamplesPerPixel);
   center = LookFrom;
@@ -427,7 +431,9 @@ void Camera::Initialize() {   // camera.go:286-344 (static camera)
   double h = std::tan(theta / 2);
   double vh = 2 * h * FocusDist;
   double vw = vh * (double(ImageWidth) / double(ImageHeight));
-  w = center.Sub(LookAt).Unit();
+  viewportHeight = vh;
+  viewportWidth = vw;
+  w = FreeCamera ? Forward.Neg() : center.Sub(LookAt).Unit();
   u = Cross(Vup, w).Unit();
   v = Cross(w, u);
   Vec3 vu = u.Scale(vw), vv = v.Neg().Scale(vh);
@@ -457,6 +463,16 @@ rt_camera_desc Camera::desc() const {
   d.phantom_hdri = PhantomHDRI;
   d.camera_motion = CameraMotion;
   d.free_camera = FreeCamera;
+  put3(d.center_motion_orig, centerMotionOrig);
+  put3(d.center_motion_dir, centerMotionDir);
+  put3(d.look_at_motion_orig, lookAtMotionOrig);
+  put3(d.look_at_motion_dir, lookAtMotionDir);
+  put3(d.vup, Vup);
+  put3(d.forward, Forward);
+  d.viewport_width = viewportWidth;
+  d.viewport_height = viewportHeight;
+  d.focus_dist = FocusDist;
+  d.defocus_radius = FocusDist * std::tan(DegreesToRadians(DefocusAngle / 2));   // camera.go:356
   return d;
 }
 
@@ -826,6 +842,56 @@ static bool hdri_scene(const SceneOptions& o, Scene& s, std::string& err, bool w
   return true;
 }
 
+static Scene checkered_spheres_scene() {   // scenes.go:132-170
+  Scene s;
+  s.world = NewHittableList();
+  auto checker = NewLambertianTexture(NewCheckerTextureFromColors(0.32, {0.2, 0.3, 0.1}, {0.9, 0.9, 0.9}));
+  s.world->Add(NewSphere({0, -10, 0}, 10, checker));
+  s.world->Add(NewSphere({0, 10, 0}, 10, checker));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(600, 16.0 / 9.0).SetQuality(100, 50).SetPosition({13, 2, 3}, {0, 0, 0}, {0, 1, 0})
+      .SetLens(20, 0, 10).EnableSkyGradient(true).Build();
+  return s;
+}
+
+static Scene glossy_metal_scene() {   // scenes.go:564-604 (GlossyMetalTest)
+  Scene s;
+  s.world = NewHittableList();
+  s.world->Add(NewPlane({0, 0, 0}, {0, 1, 0}, NewLambertian({0.5, 0.5, 0.5})));
+  s.world->Add(NewSphere({-2.5, 1, 0}, 1.0, NewMetal({0.8, 0.6, 0.2}, 0.0)));
+  s.world->Add(NewSphere({0, 1, 0}, 1.0, NewMetal({0.8, 0.6, 0.2}, 0.2)));
+  s.world->Add(NewSphere({2.5, 1, 0}, 1.0, NewMetal({0.8, 0.6, 0.2}, 0.5)));
+  auto area = NewQuad({-2, 5, -2}, {4, 0, 0}, {0, 0, 4}, NewDiffuseLight(NewSolidColor({4, 4, 4})));
+  s.world->Add(area);
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(640, 16.0 / 9.0).SetQuality(100, 10).SetPosition({0, 2, 10}, {0, 1, 0}, {0, 1, 0})
+      .SetLens(40, 0, 10).SetBackground({0, 0, 0}).AddLight(area).Build();
+  return s;
+}
+
+static Scene cornell_glossy_scene() {   // scenes.go:606-712 (CornellBoxGlossy)
+  Scene s;
+  s.world = NewHittableList();
+  auto white = NewLambertian({0.73, 0.73, 0.73});
+  auto red = NewLambertian({0.65, 0.05, 0.05});
+  auto green = NewLambertian({0.12, 0.45, 0.15});
+  s.world->Add(NewQuad({555, 0, 0}, {0, 555, 0}, {0, 0, 555}, green));
+  s.world->Add(NewQuad({0, 0, 0}, {0, 555, 0}, {0, 0, 555}, red));
+  s.world->Add(NewQuad({0, 0, 0}, {555, 0, 0}, {0, 0, 555}, white));
+  s.world->Add(NewQuad({555, 555, 555}, {-555, 0, 0}, {0, 0, -555}, white));
+  s.world->Add(NewQuad({0, 0, 555}, {555, 0, 0}, {0, 555, 0}, white));
+  auto area = NewQuad({213, 554, 227}, {130, 0, 0}, {0, 0, 105}, NewDiffuseLight(NewSolidColor({15, 15, 15})));
+  s.world->Add(area);
+  s.world->Add(NewSphere({150, 100, 400}, 100, NewMetal({1.0, 0.84, 0.0}, 0.05)));
+  s.world->Add(NewSphere({278, 100, 400}, 100, NewMetal({1.0, 0.84, 0.0}, 0.15)));
+  s.world->Add(NewSphere({410, 100, 400}, 100, NewMetal({0.95, 0.95, 0.98}, 0.25)));
+  s.world->Add(NewSphere({278, 130, 180}, 130, NewDielectric(1.5)));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(600, 1.0).SetQuality(200, 5).SetPosition({278, 278, -800}, {278, 200, 200}, {0, 1, 0})
+      .SetLens(40, 0, 10).SetBackground({0, 0, 0}).AddLight(area).Build();
+  return s;
+}
+
 static Scene quads_scene() {   // scenes.go:274-313
   Scene s;
   s.world = NewHittableList();
@@ -906,6 +972,9 @@ bool MakeScene(const std::string& name, const SceneOptions& opt, Scene& out, std
   else if (name == "cornell-lucy") { if (!cornell_lucy(opt, out, err)) return false; }
   else if (name == "hdri-test") { if (!hdri_scene(opt, out, err, false)) return false; }
   else if (name == "hdri-nee") { if (!hdri_scene(opt, out, err, true)) return false; }
+  else if (name == "checkered-spheres") out = checkered_spheres_scene();
+  else if (name == "glossy-metal") out = glossy_metal_scene();
+  else if (name == "cornell-glossy") out = cornell_glossy_scene();
   else if (name == "quads") out = quads_scene();
   else if (name == "primitives") out = primitives_scene();
   else if (name == "perlin") out = perlin_scene(opt.seed);

@@ -282,6 +282,8 @@ struct Camera {              // camera.go:18-57, NewCamera :63-83
   double Vfov = 90;
   Point3 LookFrom{0, 0, 0}, LookAt{0, 0, -1};
   Vec3 Vup{0, 1, 0};
+  Point3 LookFrom2{0, 0, 0}, LookAt2{0, 0, 0};
+  Vec3 Forward{0, 0, -1};
   double DefocusAngle = 0, FocusDist = 1;
   bool CameraMotion = false, FreeCamera = false, UseSkyGradient = false, PhantomHDRI = false;
   Color Background{0, 0, 0};
@@ -289,6 +291,8 @@ struct Camera {              // camera.go:18-57, NewCamera :63-83
   std::shared_ptr<HDRIEnvironment> Environment;
   // Initialize() outputs
   Point3 center, pixel00Loc; Vec3 pixelDeltaU, pixelDeltaV, u, v, w, defocusDiskU, defocusDiskV;
+  Point3 centerMotionOrig, lookAtMotionOrig; Vec3 centerMotionDir, lookAtMotionDir;
+  double viewportHeight = 0, viewportWidth = 0;
   double pixelsSamplesScale = 0;
 
   Camera& SetResolution(int width, double aspect) { ImageWidth = width; AspectRatio = aspect; return *this; }
@@ -299,6 +303,10 @@ struct Camera {              // camera.go:18-57, NewCamera :63-83
   Camera& EnableSkyGradient(bool e) { UseSkyGradient = e; return *this; }
   Camera& SetPhantomHDRI(bool p) { PhantomHDRI = p; return *this; }
   Camera& AddLight(HittablePtr l) { Lights.push_back(std::move(l)); return *this; }
+  Camera& SetMotion(Point3 from2, Point3 at2) { LookFrom2 = from2; LookAt2 = at2; CameraMotion = true; return *this; }
+  Camera& EnableFreeCamera(Point3 pos, Vec3 fwd, Vec3 up) {   // camera.go:226-232
+    LookFrom = pos; Forward = fwd.Unit(); Vup = up.Unit(); FreeCamera = true; return *this;
+  }
   Camera& Build() { Initialize(); return *this; }
   void Initialize();         // camera.go:286-344
   rt_camera_desc desc() const;

@@ -123,6 +123,14 @@ int rts_scene_create(const char* name, const rts_scene_options* opt, rts_scene**
     delete s;
     return RT_ERR_INVALID;
   }
+  if (opt && (opt->camera_motion || opt->free_camera)) {   // camera.go:204-232, then Build()
+    rt::Camera& c = *s->scene.camera;
+    if (opt->camera_motion)
+      c.SetMotion({opt->look_from2[0], opt->look_from2[1], opt->look_from2[2]},
+                  {opt->look_at2[0], opt->look_at2[1], opt->look_at2[2]});
+    if (opt->free_camera) c.EnableFreeCamera(c.LookFrom, {opt->forward[0], opt->forward[1], opt->forward[2]}, c.Vup);
+    c.Initialize();
+  }
   // main.go:77 — the renderer receives NewBVHNodeFromList(world).
   auto bvh = rt::NewBVHNodeFromList(*s->scene.world);
   s->em.build(bvh, *s->scene.camera);

@@ -105,22 +105,9 @@ __global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, PathStr
     const uint32_t pix = a.pixels[pi];
     const int px = int(pix % uint32_t(cam.width)), py = int(pix / uint32_t(cam.width));
     const uint32_t key = path_key(a.seed, pix, sample_base + sm);
-    // GetRay camera.go:368-388
-    float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
-    float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
-    float time = rnd(key, ctr(0, DOM_CAMERA, 2));
-    V3 ps = add(add(ld3(cam.pixel00), scale(ld3(cam.du), float(px) + offx)), scale(ld3(cam.dv), float(py) + offy));
-    V3 ro = ld3(cam.center);
-    if (cam.defocus) {
-      V3 p = mk(0.0f, 0.0f, 0.0f);
-      for (int k = 0; k < MAX_DISK_TRIES; ++k) {
-        uint32_t c = ctr(0, DOM_CAMERA, 3u + 2u * k);
-        float x = -1.0f + 2.0f * rnd(key, c), y = -1.0f + 2.0f * rnd(key, c + 1u);
-        if (x * x + y * y + 0.0f * 0.0f < 1.0f) { p = mk(x, y, 0.0f); break; }
-      }
-      ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
-    }
-    V3 rd = sub(ps, ro);
+    V3 ro, rd;
+    float time;
+    get_ray(cam, px, py, key, ro, rd, time);   // GetRay camera.go:368-434
     stnt(&s.o[i], make_float4(ro.x, ro.y, ro.z, time));
     stnt(&s.d[i], make_float4(rd.x, rd.y, rd.z, asf(key)));
     stnt(&s.beta[i], make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true))));

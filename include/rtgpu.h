@@ -173,8 +173,20 @@ typedef struct rt_camera_desc {
   double background[3];      /* c.Background                                 */
   int32_t use_sky_gradient;  /* c.UseSkyGradient                             */
   int32_t phantom_hdri;      /* c.PhantomHDRI                                */
-  int32_t camera_motion;     /* c.CameraMotion (unsupported: must be 0)      */
-  int32_t free_camera;       /* c.FreeCamera   (unsupported: must be 0)      */
+  int32_t camera_motion;     /* c.CameraMotion                               */
+  int32_t free_camera;       /* c.FreeCamera                                 */
+  /* GetRay's slow path (camera.go:390-434), read only when camera_motion or
+   * free_camera is set: the basis is rebuilt per sample at rayTime.       */
+  double center_motion_orig[3];  /* c.centerMotion.orig (LookFrom)          */
+  double center_motion_dir[3];   /* c.centerMotion.dir (LookFrom2-LookFrom or 0) */
+  double look_at_motion_orig[3]; /* c.lookAtMotion.orig (LookAt)            */
+  double look_at_motion_dir[3];  /* c.lookAtMotion.dir (LookAt2-LookAt or 0) */
+  double vup[3];             /* c.Vup                                        */
+  double forward[3];         /* c.Forward (free camera: w = -Forward)        */
+  double viewport_width;     /* c.viewportWidth  (camera.go:311)             */
+  double viewport_height;    /* c.viewportHeight (camera.go:310)             */
+  double focus_dist;         /* c.FocusDist                                  */
+  double defocus_radius;     /* FocusDist*tan(DefocusAngle/2) (camera.go:356) */
 } rt_camera_desc;
 
 /* ---- render call ----------------------------------------------------------- */

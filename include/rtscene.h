@@ -28,12 +28,18 @@ typedef struct rts_scene_options {
   const char* asset_dir;/* directory holding hdri/ (NULL: "assets")           */
   const char* obj_path; /* Lucy OBJ (NULL: deterministic synthetic stand-in)  */
   int32_t lucy_rings, lucy_cols; /* synthetic Lucy resolution (0: 350 x 400)  */
+  int32_t camera_motion;   /* 1: Camera.SetMotion(look_from2, look_at2)     */
+  double look_from2[3], look_at2[3];
+  int32_t free_camera;     /* 1: Camera.EnableFreeCamera(LookFrom, forward, Vup) */
+  double forward[3];
 } rts_scene_options;
 
 typedef struct rts_scene rts_scene;
 
 /* name: "simple" | "random" | "cornell" | "cornell-lucy" | "hdri-test" |
- *       "cornell-smoke" | "hdri-nee" (test-only: HDRI + quad light).
+ *       "cornell-smoke" | "quads" | "primitives" | "perlin" | "earth" |
+ *       "checkered-spheres" | "glossy-metal" | "cornell-glossy" |
+ *       "hdri-nee" (test-only: HDRI + quad light).
  * The world is wrapped in NewBVHNodeFromList like main.go:77.            */
 int rts_scene_create(const char* name, const rts_scene_options* opt, rts_scene** out, char* err, int32_t errlen);
 void rts_scene_destroy(rts_scene* s);

@@ -230,7 +230,6 @@ static void default_buckets(int W, int H, rt_bucket** out, int* n) {   /* genera
 int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* cam, const rt_render_params* p, int fp32,
                   int nthreads, double* accum) {
   if (!scene || !cam || !p || !accum) return RT_ERR_INVALID;
-  if (cam->camera_motion || cam->free_camera) return RT_ERR_UNSUPPORTED;
   OScene os;
   int rc = oscene_init(&os, scene);
   if (rc) return rc;

@@ -59,6 +59,9 @@ typedef struct {
   REAL env_rot;
   REAL cam_center[3], cam_p00[3], cam_du[3], cam_dv[3], cam_disk_u[3], cam_disk_v[3], cam_bg[3];
   int cam_defocus, cam_sky, cam_phantom, cam_max_depth;
+  int cam_slow, cam_free, cam_w, cam_h;                          /* GetRay slow path (camera.go:390-434) */
+  REAL cam_corig[3], cam_cdir[3], cam_laorig[3], cam_ladir[3], cam_vup[3], cam_fwd[3];
+  REAL cam_vw, cam_vh, cam_focus, cam_rad;
 } FN(OS);
 
 static int FN(prep)(FN(OS)* S, const OScene* os, const rt_camera_desc* cam) {
@@ -101,6 +104,22 @@ static int FN(prep)(FN(OS)* S, const OScene* os, const rt_camera_desc* cam) {
   S->cam_sky = cam->use_sky_gradient != 0;
   S->cam_phantom = cam->phantom_hdri != 0;
   S->cam_max_depth = cam->max_depth;
+  S->cam_slow = cam->camera_motion || cam->free_camera;
+  S->cam_free = cam->free_camera != 0;
+  S->cam_w = cam->image_width;
+  S->cam_h = cam->image_height;
+  for (int a = 0; a < 3; ++a) {
+    S->cam_corig[a] = (REAL)cam->center_motion_orig[a];
+    S->cam_cdir[a] = (REAL)cam->center_motion_dir[a];
+    S->cam_laorig[a] = (REAL)cam->look_at_motion_orig[a];
+    S->cam_ladir[a] = (REAL)cam->look_at_motion_dir[a];
+    S->cam_vup[a] = (REAL)cam->vup[a];
+    S->cam_fwd[a] = (REAL)cam->forward[a];
+  }
+  S->cam_vw = (REAL)cam->viewport_width;
+  S->cam_vh = (REAL)cam->viewport_height;
+  S->cam_focus = (REAL)cam->focus_dist;
+  S->cam_rad = (REAL)cam->defocus_radius;
   return 0;
 }
 
@@ -707,6 +726,46 @@ static V3R FN(ray_color)(FN(TC)* c, FN(Ray) r, int depth, uint32_t bounce, int a
   return FN(add)(FN(add)(Le, direct), ind);
 }
 
+/* RandomInUnitDisk (vec3.go:66-77) on the camera counters */
+static V3R FN(disk_point)(FN(TC)* c) {
+  V3R p = FN(mk)(0, 0, 0);
+  for (int k = 0; k < O_MAX_TRIES; ++k) {
+    uint32_t idx = 3u + 2u * (uint32_t)k;
+    REAL x = -1 + 2 * FN(rnd)(c, O_DOM_CAMERA, idx), y = -1 + 2 * FN(rnd)(c, O_DOM_CAMERA, idx + 1);
+    if (x * x + y * y + (REAL)0 * (REAL)0 < 1) { p = FN(mk)(x, y, 0); break; }
+  }
+  return p;
+}
+
+/* GetRay slow path camera.go:390-434 (CameraMotion / FreeCamera): the basis
+ * and pixel grid are rebuilt at rayTime from the cached viewport size. */
+static FN(Ray) FN(get_ray_slow)(FN(TC)* c, int i, int j, REAL ox, REAL oy, REAL tm) {
+  const FN(OS)* S = c->S;
+  V3R center = FN(add)(FN(ld3)(S->cam_corig), FN(scale)(FN(ld3)(S->cam_cdir), tm));   /* centerMotion.At */
+  V3R w;
+  if (S->cam_free) w = FN(neg)(FN(ld3)(S->cam_fwd));
+  else w = FN(unit)(FN(sub)(center, FN(add)(FN(ld3)(S->cam_laorig), FN(scale)(FN(ld3)(S->cam_ladir), tm))));
+  V3R u = FN(unit)(FN(cross)(FN(ld3)(S->cam_vup), w));
+  V3R v = FN(cross)(w, u);
+  V3R vu = FN(scale)(u, S->cam_vw);
+  V3R vv = FN(scale)(FN(neg)(v), S->cam_vh);
+  V3R du = FN(divs)(vu, (REAL)S->cam_w);
+  V3R dv = FN(divs)(vv, (REAL)S->cam_h);
+  V3R ul = FN(sub)(FN(sub)(FN(sub)(center, FN(scale)(w, S->cam_focus)), FN(divs)(vu, 2)), FN(divs)(vv, 2));
+  V3R p00 = FN(add)(ul, FN(scale)(FN(add)(du, dv), (REAL)0.5));
+  V3R ps = FN(add)(FN(add)(p00, FN(scale)(du, (REAL)i + ox)), FN(scale)(dv, (REAL)j + oy));
+  V3R ro = center;
+  if (S->cam_defocus) {
+    V3R p = FN(disk_point)(c);
+    ro = FN(add)(FN(add)(center, FN(scale)(FN(scale)(u, S->cam_rad), p.x)), FN(scale)(FN(scale)(v, S->cam_rad), p.y));
+  }
+  FN(Ray) r;
+  r.o = ro;
+  r.d = FN(sub)(ps, ro);
+  r.tm = tm;
+  return r;
+}
+
 /* GetRay camera.go:368-388 */
 static FN(Ray) FN(get_ray)(FN(TC)* c, int i, int j) {
   const FN(OS)* S = c->S;
@@ -714,16 +773,12 @@ static FN(Ray) FN(get_ray)(FN(TC)* c, int i, int j) {
   REAL ox = FN(rnd)(c, O_DOM_CAMERA, 0) - (REAL)0.5;
   REAL oy = FN(rnd)(c, O_DOM_CAMERA, 1) - (REAL)0.5;
   REAL tm = FN(rnd)(c, O_DOM_CAMERA, 2);
+  if (S->cam_slow) return FN(get_ray_slow)(c, i, j, ox, oy, tm);
   V3R ps = FN(add)(FN(add)(FN(ld3)(S->cam_p00), FN(scale)(FN(ld3)(S->cam_du), (REAL)i + ox)),
                    FN(scale)(FN(ld3)(S->cam_dv), (REAL)j + oy));
   V3R ro = FN(ld3)(S->cam_center);
   if (S->cam_defocus) {                                                      /* defocusDiskSample :354-362 */
-    V3R p = FN(mk)(0, 0, 0);
-    for (int k = 0; k < O_MAX_TRIES; ++k) {
-      uint32_t idx = 3u + 2u * (uint32_t)k;
-      REAL x = -1 + 2 * FN(rnd)(c, O_DOM_CAMERA, idx), y = -1 + 2 * FN(rnd)(c, O_DOM_CAMERA, idx + 1);
-      if (x * x + y * y + (REAL)0 * (REAL)0 < 1) { p = FN(mk)(x, y, 0); break; }
-    }
+    V3R p = FN(disk_point)(c);
     ro = FN(add)(FN(add)(ro, FN(scale)(FN(ld3)(S->cam_disk_u), p.x)), FN(scale)(FN(ld3)(S->cam_disk_v), p.y));
   }
   FN(Ray) r;

@@ -10,6 +10,7 @@
 #define __host__
 #define __device__
 #define __forceinline__ inline
+#define __noinline__ __attribute__((noinline))
 #define __global__
 #define __shared__ static
 #define __launch_bounds__(...)

@@ -61,11 +61,11 @@ def test_ctypes_mirror_matches_c_header(g, tmp_path):
              "rt_work_counts": g.RtWorkCounts, "rt_kernel_times": g.RtKernelTimes,
              "rt_scene_info": g.RtSceneInfo, "rt_camera_desc": g.RtCameraDesc,
              "rt_render_params": g.RtRenderParams, "rt_scene_desc": g.RtSceneDesc, "rt_stats": g.RtStats,
-             "rt_image": g.RtImage, "rt_perlin": g.RtPerlin}
+             "rt_image": g.RtImage, "rt_perlin": g.RtPerlin, "rts_scene_options": g.RtsSceneOptions}
     src = tmp_path / "probe.c"
     inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
     body = "".join(f'  printf("{n} %zu\\n", sizeof({n}));\n' for n in names)
-    src.write_text(f'#include <stdio.h>\n#include "rtgpu.h"\nint main(void) {{\n{body}  return 0;\n}}\n')
+    src.write_text(f'#include <stdio.h>\n#include "rtscene.h"\nint main(void) {{\n{body}  return 0;\n}}\n')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")

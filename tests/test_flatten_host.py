@@ -29,7 +29,7 @@ LIB = os.path.join(ROOT, "go-raytracing_amd", "lib")
 CSRC = os.path.join(ROOT, "go-raytracing_amd", "csrc")
 ASSETS = os.path.join(ROOT, "assets")
 SCENES = ["simple", "random", "cornell", "cornell-smoke", "cornell-lucy", "hdri-test", "hdri-nee", "quads",
-          "primitives", "perlin", "earth"]
+          "primitives", "perlin", "earth", "checkered-spheres", "glossy-metal", "cornell-glossy"]
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
 
@@ -102,7 +102,7 @@ def test_device_source_under_asan_matches_oracle(emu, O, g, tmp_path, name):
 
 @pytest.mark.parametrize("name,batch", [("simple", 0), ("cornell", 1), ("cornell-smoke", 0), ("cornell-lucy", 1),
                                         ("hdri-nee", 0), ("random", 0), ("primitives", 1), ("perlin", 0),
-                                        ("earth", 0)])
+                                        ("earth", 0), ("glossy-metal", 0), ("cornell-glossy", 1)])
 def test_wavefront_kernels_under_asan_match_oracle(wave, O, g, tmp_path, name, batch):
     spp, seed, width = 2, 77, 40
     out = tmp_path / f"{name}.f32"

@@ -25,6 +25,9 @@ SCENES = [
     ("primitives", dict(width=96)),
     ("perlin", dict(width=96)),
     ("earth", dict(width=96)),
+    ("checkered-spheres", dict(width=96)),
+    ("glossy-metal", dict(width=96)),
+    ("cornell-glossy", dict(width=64)),
 ]
 
 
@@ -47,7 +50,7 @@ def test_primary_hits_bit_exact(g, O, ctx, name, kw):
         assert mism.size <= allowed, f"{name}: {mism.size} mismatches, first {mism[:5]}"
         same = (tg == to) & (pg == po) & (tg >= 0)
         if name in ("simple", "random", "cornell-lucy", "hdri-test", "hdri-nee", "quads", "primitives", "perlin",
-                    "earth"):
+                    "earth", "checkered-spheres", "glossy-metal", "cornell-glossy"):
             assert np.array_equal(t_g[same], t_o[same].astype(np.float32)), f"{name}: hit t differs"
         assert (tg >= 0).any()
 
@@ -150,16 +153,6 @@ def test_overwrite_only_bucket_pixels(g, ctx):
     ctx.render(cam, g.make_params(2, 10, seed=3, buckets=[(0, 0, 16, 8)]), acc)
     assert (acc[:8, :16] != -7.0).all()
     assert (acc[8:] == -7.0).all() and (acc[:, 16:] == -7.0).all()
-
-
-def test_camera_motion_unsupported(g, ctx):
-    s = g.Scene("simple", width=32)
-    cam = s.camera
-    ctx.upload(s.desc)
-    cam.camera_motion = 1
-    with pytest.raises(g.RTError) as e:
-        ctx.render(cam, g.make_params(1, 3))
-    assert e.value.code == -2
 
 
 def test_count_work(g, ctx):
