@@ -1,10 +1,11 @@
 #!/bin/bash
-# GPU parity suite + bench A/B of the two BLAS builders (one gpurun call).
+# A/B the default bench workload over values of one environment variable:
+#   tools/gpu_ab.sh VAR v1 v2 ...   [BENCH_ARGS="--scene random"]
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -2 gpurun_out/pytest_gpu.log
-for b in reference sah; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --blas $b > gpurun_out/bench_$b.json 2> gpurun_out/bench_$b.err || { tail -20 gpurun_out/bench_$b.err; exit 1; }
-  python3 -c "import json;d=json.load(open('gpurun_out/bench_$b.json'));print('$b',d['value'],d['roofline']['frac'],{k:v['ms_total'] for k,v in d['kernels'].items()},d['work_per_sample'])"
+var=$1; shift
+for v in "$@"; do
+  tag=${var}_${v}
+  env "$var=$v" timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $BENCH_ARGS > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err || { tail -20 gpurun_out/ab_$tag.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/ab_$tag.json'));w=d['work_per_sample'];print('$tag',d['value'],d['roofline']['frac'],{k:v['ms_total'] for k,v in d['kernels'].items()},'nodes',w['node_visits'],'quads',w['quad_tests'],'tris',w['tri_tests'],'inst',w['instance_visits'])"
 done
