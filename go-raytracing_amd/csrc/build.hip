@@ -183,7 +183,8 @@ __global__ __launch_bounds__(256) void k_collapse(const Entry* in, uint32_t n_in
       const uint32_t first = (id & kLeafBit) ? (id & ~kLeafBit) : range[id].x;
       const uint32_t li = leaves_base + atomicAdd(leaf_ctr, 1u);
       leaves[li] = DLeaf{tri_first + first, make_leaf_info(int(cnt), PK_TRI, 1)};
-      o.item[q] = (ITEM_LEAF << ITEM_SHIFT) | li;
+      o.item[q] = cnt <= uint32_t(kInlineTriMax) ? tri_leaf_item(tri_first + first, int(cnt))
+                                                 : ((ITEM_LEAF << ITEM_SHIFT) | li);
       atomicMax(max_need, need);
     } else {
       const uint32_t slot = nodes_base + atomicAdd(node_ctr, 1u);

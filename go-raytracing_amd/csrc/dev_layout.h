@@ -29,9 +29,20 @@ enum : uint32_t {
   ITEM_LEAF = 1u,       // leaf record index
   ITEM_INSTANCE = 2u,   // enter instance: index = instance id
   ITEM_INST_END = 3u,   // leave instance: restore the world-space ray
+  ITEM_TRI1 = 4u,       // tags 4..7: inline triangle leaf of (tag - 3) triangles
+                        // at index.. (no DLeaf fetch: one dependent load less)
 };
 constexpr int ITEM_SHIFT = 28;
 constexpr uint32_t ITEM_MASK = (1u << ITEM_SHIFT) - 1u;
+constexpr int kInlineTriMax = 4;
+__host__ __device__ inline uint32_t tri_leaf_item(uint32_t first, int n) {
+  return ((ITEM_TRI1 + uint32_t(n) - 1u) << ITEM_SHIFT) | first;
+}
+// Leaf-like items (a DLeaf record or an inline triangle leaf).
+__host__ __device__ inline bool item_is_leaf(uint32_t item) {
+  const uint32_t tag = item >> ITEM_SHIFT;
+  return tag == ITEM_LEAF || (tag >= ITEM_TRI1 && tag < ITEM_TRI1 + uint32_t(kInlineTriMax));
+}
 
 // Primitive reference kinds (leaf "kind" field and ref tags).
 enum : int {

@@ -518,7 +518,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
   T.item = sc.tlas.root_item;
   if ((T.item >> ITEM_SHIFT) != ITEM_NODE) {
     T.lf = T.item;
-    T.item = ((T.lf >> ITEM_SHIFT) == ITEM_LEAF) ? ITEM_NONE : ITEM_POP;
+    T.item = item_is_leaf(T.lf) ? ITEM_NONE : ITEM_POP;
   }
   return TRAV_RUNNING;
 }
@@ -539,7 +539,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   };
   auto postpone = [&]() {
     T.lf = T.item;
-    T.item = ((T.lf >> ITEM_SHIFT) == ITEM_LEAF) ? pop() : ITEM_POP;
+    T.item = item_is_leaf(T.lf) ? pop() : ITEM_POP;
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
@@ -584,8 +584,10 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   // ---------------- phase 2: leaves, instance entry / exit
   while (T.lf != ITEM_NONE) {
     const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
-    if (tag == ITEM_LEAF) {
-      const DLeaf leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
+    if (tag == ITEM_LEAF || tag >= ITEM_TRI1) {
+      DLeaf leaf;
+      if (tag == ITEM_LEAF) leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
+      else { leaf.first = idx; leaf.info = make_leaf_info(int(tag - ITEM_TRI1) + 1, PK_TRI, 1); }
       const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
       const bool world = T.cur_ref < 0;
       for (int k = 0; k < n; ++k) {

@@ -1046,6 +1046,19 @@ struct Flattener {
       b.root_item = collapse4(b.root_item, n);
       S.blas_need4 = std::max(S.blas_need4, n);
     }
+    // Triangle leaves tested once become inline items (the node slot holds
+    // first index + count; BLAS roots keep their DLeaf, volumes read it).
+    for (DNode4& o : S.nodes4)
+      for (uint32_t& it : o.item) it = inline_leaf(it);
+  }
+  uint32_t inline_leaf(uint32_t item) const {
+    if ((item >> ITEM_SHIFT) != ITEM_LEAF || item == empty_leaf) return item;
+    const DLeaf& L = S.leaves[item & ITEM_MASK];
+    const int n = leaf_count(L.info);
+    if (leaf_kind(L.info) != PK_TRI || leaf_ntests(L.info) != 1 || n < 1 || n > kInlineTriMax ||
+        uint64_t(L.first) + uint64_t(n) > uint64_t(ITEM_MASK))
+      return item;
+    return tri_leaf_item(L.first, n);
   }
 
   int run() {

@@ -26,6 +26,8 @@ static void check_item(const HostScene& S, uint32_t it, const char* where) {
   const uint32_t tag = it >> ITEM_SHIFT, idx = it & ITEM_MASK;
   if (tag == ITEM_NODE) CHECK(idx < S.nodes4.size(), std::string(where) + ": node item out of range");
   else if (tag == ITEM_LEAF) CHECK(idx < S.leaves.size(), std::string(where) + ": leaf item out of range");
+  else if (item_is_leaf(it))
+    CHECK(size_t(idx) + (tag - ITEM_TRI1) + 1 <= S.tris.size(), std::string(where) + ": inline triangle leaf out of range");
   else CHECK(false, std::string(where) + ": bad item tag");
 }
 
@@ -63,7 +65,7 @@ int main(int argc, char** argv) {
   // it was collapsed from (non-empty child slots only), and every child box
   // of a BVH4 node contains the boxes inside that child.
   {
-    std::vector<int> seen(S.leaves.size(), 0);
+    std::vector<int> seen(S.leaves.size(), 0), seen_tri(S.tris.size(), 0);
     std::vector<uint32_t> st;
     auto walk = [&](uint32_t root) {
       st.assign(1, root);
@@ -71,6 +73,10 @@ int main(int argc, char** argv) {
         const uint32_t it = st.back();
         st.pop_back();
         if ((it >> ITEM_SHIFT) == ITEM_LEAF) { seen[it & ITEM_MASK]++; continue; }
+        if (item_is_leaf(it)) {   // inline triangle leaf
+          if ((it & ITEM_MASK) < S.tris.size()) seen_tri[it & ITEM_MASK]++;
+          continue;
+        }
         if ((it >> ITEM_SHIFT) != ITEM_NODE || (it & ITEM_MASK) >= S.nodes4.size()) continue;
         const DNode4& n = S.nodes4[it & ITEM_MASK];
         for (int c = 0; c < 4; ++c)
@@ -92,8 +98,11 @@ int main(int argc, char** argv) {
     // every leaf child of a BVH2 node is reached through the BVH4
     for (const DNode& n : S.nodes)
       for (uint32_t it : {n.litem, n.ritem})
-        if ((it >> ITEM_SHIFT) == ITEM_LEAF && (it & ITEM_MASK) != 0u)
-          CHECK(seen[it & ITEM_MASK] > 0, "BVH2 leaf not reached through the BVH4");
+        if ((it >> ITEM_SHIFT) == ITEM_LEAF && (it & ITEM_MASK) != 0u) {
+          const DLeaf& L = S.leaves[it & ITEM_MASK];
+          const bool inl = leaf_kind(L.info) == PK_TRI && L.first < S.tris.size() && seen_tri[L.first] > 0;
+          CHECK(seen[it & ITEM_MASK] > 0 || inl, "BVH2 leaf not reached through the BVH4");
+        }
   }
   int culled = 0;
   for (size_t li = 0; li < S.leaves.size(); ++li) {
