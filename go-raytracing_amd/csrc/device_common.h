@@ -105,6 +105,7 @@ __device__ __forceinline__ V3 random_unit_vector(uint32_t key, uint32_t bounce, 
 struct TRay {
   V3 o, d, inv;
 };
+typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ TRay make_tray(V3 o, V3 d) {
   TRay r; r.o = o; r.d = d;
   r.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // AABB.Hit adinv (aabb.go:64)
@@ -544,17 +545,29 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
     const float4* np = reinterpret_cast<const float4*>(sc.nodes + GIX(T.item & ITEM_MASK, sc.n_nodes, 9));
-    const float4 xl = np[0], xh = np[1], yl = np[2], yh = np[3], zl = np[4], zh = np[5];
+    // box_hit for the four children at once: the near / far plane of each
+    // axis is picked by the load address (the ray's direction signs) instead
+    // of per-child selects — the same operations as box_hit, bit for bit.
+    const uint32_t sxn = __float_as_uint(T.cr.inv.x) >> 31, syn = __float_as_uint(T.cr.inv.y) >> 31,
+                   szn = __float_as_uint(T.cr.inv.z) >> 31;
+    const float4 nx = np[sxn], fx = np[1u - sxn], ny = np[2u + syn], fy = np[3u - syn];
+    const float4 nz = np[4u + szn], fz = np[5u - szn];
     const uint4 it = reinterpret_cast<const uint4*>(np)[6];
     if (kCount) cnt.nodes++;
     const float hi = kAny ? T.tmax : best.t;
-    // entry distance per child, +inf when missed
-    float t0, t1, t2, t3;
     const float inf = __builtin_inff();
-    t0 = box_hit(xl.x, xh.x, yl.x, yh.x, zl.x, zh.x, T.cr, T.tmin, hi, t0) ? t0 : inf;
-    t1 = box_hit(xl.y, xh.y, yl.y, yh.y, zl.y, zh.y, T.cr, T.tmin, hi, t1) ? t1 : inf;
-    t2 = box_hit(xl.z, xh.z, yl.z, yh.z, zl.z, zh.z, T.cr, T.tmin, hi, t2) ? t2 : inf;
-    t3 = box_hit(xl.w, xh.w, yl.w, yh.w, zl.w, zh.w, T.cr, T.tmin, hi, t3) ? t3 : inf;
+    auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
+      const float tx0 = (nxp - T.cr.o.x) * T.cr.inv.x, tx1 = (fxp - T.cr.o.x) * T.cr.inv.x;
+      const float ty0 = (nyp - T.cr.o.y) * T.cr.inv.y, ty1 = (fyp - T.cr.o.y) * T.cr.inv.y;
+      const float tz0 = (nzp - T.cr.o.z) * T.cr.inv.z, tz1 = (fzp - T.cr.o.z) * T.cr.inv.z;
+      const float a = fmaxf(fmaxf(fmaxf(T.tmin, tx0), ty0), tz0);
+      const float b = fminf(fminf(fminf(hi, tx1), ty1), tz1);
+      return b > a ? a : inf;
+    };
+    float t0 = child_t(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x);
+    float t1 = child_t(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y);
+    float t2 = child_t(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z);
+    float t3 = child_t(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w);
     const int nh = int(t0 < inf) + int(t1 < inf) + int(t2 < inf) + int(t3 < inf);
     if (nh == 0) {
       T.item = pop();
@@ -568,6 +581,8 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
       };
       cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2);
+      // (a branch-free three-slot LDS write when no spill is possible measured
+      // 0.5 % slower than these guarded pushes)
       if (nh > 3 && !push(i3)) return TRAV_DONE;
       if (nh > 2 && !push(i2)) return TRAV_DONE;
       if (nh > 1 && !push(i1)) return TRAV_DONE;
