@@ -327,7 +327,8 @@ struct Flattener {
         if (P[i].c[a] > cb.b[2 * a + 1]) cb.b[2 * a + 1] = P[i].c[a];
       }
     }
-    constexpr int kBins = 16;
+    static constexpr int kMaxBins = 64;
+    static const int kBins = [] { const char* v = std::getenv("RTG_SAH_BINS"); return v ? std::min(kMaxBins, std::max(2, std::atoi(v))) : 32; }();
     // Leaves of at most 2 primitives; a node visit ~ two triangle tests.
     // Measured on CornellBoxLucy (Msamples/s): leaf<=1 961, <=2 1002, <=3 991,
     // <=4 976, <=6 969; kTrav 0.5/1/2/3 at leaf<=2: 987/1003/1002/-.
@@ -340,16 +341,16 @@ struct Flattener {
     for (int a = 0; a < 3; ++a) {
       const double lo = cb.b[2 * a], ext = cb.b[2 * a + 1] - lo;
       if (!(ext > 0.0)) continue;
-      Box bb[kBins];
-      int cnt[kBins] = {0};
+      Box bb[kMaxBins];
+      int cnt[kMaxBins] = {0};
       for (int i = b; i < e; ++i) {
         int k = int((P[i].c[a] - lo) / ext * kBins);
         k = std::min(std::max(k, 0), kBins - 1);
         cnt[k]++;
         grow(bb[k], P[i]);
       }
-      double right_area[kBins];
-      int right_cnt[kBins];
+      double right_area[kMaxBins];
+      int right_cnt[kMaxBins];
       Box acc;
       int c = 0;
       for (int k = kBins - 1; k > 0; --k) {
