@@ -534,9 +534,13 @@ template <bool kAny, bool kCount, bool kVol>
 __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
   Best& best = T.best;
   auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return S.pop(T.sp); };
+  // The host bounds the stack need (flatten: stack_needed <= kStackMax), so an
+  // overflow is an internal error: flagged for the host, the entry dropped,
+  // and no early exit in the push sequence.
   auto push = [&](uint32_t v) -> bool {
-    if (T.sp >= S.cap + S.spill_cap) { *err = 1; return false; }
-    S.push(T.sp, v); ++T.sp; return true;
+    if (T.sp < S.cap + S.spill_cap) { S.push(T.sp, v); ++T.sp; }
+    else *err = 1;
+    return true;
   };
   auto postpone = [&]() {
     T.lf = T.item;
@@ -544,15 +548,18 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
-    const float4* np = reinterpret_cast<const float4*>(sc.nodes + GIX(T.item & ITEM_MASK, sc.n_nodes, 9));
+    // 32-bit byte offsets from the uniform node base (saddr + voffset loads)
+    const uint32_t nb = GIX(T.item & ITEM_MASK, sc.n_nodes, 9) << 7;
+    const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
+    auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };
     // box_hit for the four children at once: the near / far plane of each
     // axis is picked by the load address (the ray's direction signs) instead
     // of per-child selects — the same operations as box_hit, bit for bit.
-    const uint32_t sxn = __float_as_uint(T.cr.inv.x) >> 31, syn = __float_as_uint(T.cr.inv.y) >> 31,
-                   szn = __float_as_uint(T.cr.inv.z) >> 31;
-    const float4 nx = np[sxn], fx = np[1u - sxn], ny = np[2u + syn], fy = np[3u - syn];
-    const float4 nz = np[4u + szn], fz = np[5u - szn];
-    const uint4 it = reinterpret_cast<const uint4*>(np)[6];
+    const uint32_t sxo = (__float_as_uint(T.cr.inv.x) >> 27) & 16u, syo = (__float_as_uint(T.cr.inv.y) >> 27) & 16u,
+                   szo = (__float_as_uint(T.cr.inv.z) >> 27) & 16u;
+    const float4 nx = ldn(nb + sxo), fx = ldn(nb + (16u - sxo)), ny = ldn(nb + (32u + syo)), fy = ldn(nb + (48u - syo));
+    const float4 nz = ldn(nb + (64u + szo)), fz = ldn(nb + (80u - szo));
+    const uint4 it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
     if (kCount) cnt.nodes++;
     const float hi = kAny ? T.tmax : best.t;
     const float inf = __builtin_inff();
