@@ -537,10 +537,9 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   // The host bounds the stack need (flatten: stack_needed <= kStackMax), so an
   // overflow is an internal error: flagged for the host, the entry dropped,
   // and no early exit in the push sequence.
-  auto push = [&](uint32_t v) -> bool {
+  auto push = [&](uint32_t v) {
     if (T.sp < S.cap + S.spill_cap) { S.push(T.sp, v); ++T.sp; }
     else *err = 1;
-    return true;
   };
   auto postpone = [&]() {
     T.lf = T.item;
@@ -575,24 +574,23 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     float t1 = child_t(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y);
     float t2 = child_t(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z);
     float t3 = child_t(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w);
-    const int nh = int(t0 < inf) + int(t1 < inf) + int(t2 < inf) + int(t3 < inf);
-    if (nh == 0) {
+    // near-to-far order (5-comparator network, missed children sort last as
+    // +inf); visit the nearest, push the other hit children far first
+    uint32_t i0 = it.x, i1 = it.y, i2 = it.z, i3 = it.w;
+    auto cs = [](float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
+      const bool sw = tb < ta;
+      const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
+      const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
+    };
+    cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2);
+    if (!(t0 < inf)) {
       T.item = pop();
     } else {
-      // near-to-far order (5-comparator network); visit the nearest, push the
-      // other hit children far first
-      uint32_t i0 = it.x, i1 = it.y, i2 = it.z, i3 = it.w;
-      auto cs = [](float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
-        const bool sw = tb < ta;
-        const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
-        const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
-      };
-      cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2);
       // (a branch-free three-slot LDS write when no spill is possible measured
       // 0.5 % slower than these guarded pushes)
-      if (nh > 3 && !push(i3)) return TRAV_DONE;
-      if (nh > 2 && !push(i2)) return TRAV_DONE;
-      if (nh > 1 && !push(i1)) return TRAV_DONE;
+      if (t3 < inf) push(i3);
+      if (t2 < inf) push(i2);
+      if (t1 < inf) push(i1);
       T.item = i0;
     }
     // leaving an instance with nothing postponed: restore the world ray inline
@@ -639,7 +637,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           float tn = 0.0f;
           if (kCount) cnt.ibox++;
           if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : best.t, tn)) continue;
-          if (!push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos))) return TRAV_DONE;
+          push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos));
           continue;
         } else if (kVol && pk == PK_VOLUME) {
           ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), T.time, T.tmin, kAny ? T.tmax : best.t,
@@ -669,8 +667,8 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         enter = box_hit(bb.box[0], bb.box[1], bb.box[2], bb.box[3], bb.box[4], bb.box[5], orr, T.tmin,
                         kAny ? T.tmax : best.t, tn);
       if (enter) {
-        if (T.item < ITEM_POP && !push(T.item)) return TRAV_DONE;
-        if (!push(ITEM_INST_END << ITEM_SHIFT)) return TRAV_DONE;
+        if (T.item < ITEM_POP) push(T.item);
+        push(ITEM_INST_END << ITEM_SHIFT);
         T.cr = orr; T.cur_ref = int(idx);
         T.item = bb.root_item;
       }
