@@ -83,13 +83,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one rank per GPU; RTGPU_BENCH_BACKEND=gloo (with ranks sharing the
+    # visible GPUs) rehearses the multi-rank path on a one-GPU box
+    backend = os.environ.get("RTGPU_BENCH_BACKEND", "nccl")
+    ndev = max(torch.cuda.device_count(), 1)
+    dev_index = local % ndev if world > 1 else 0
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", dev_index)
 
     import __graft_entry__ as ge
     g = ge.load_package()
@@ -107,7 +112,7 @@ def main():
     scene = g.Scene(args.scene, **scene_kw)
     cam = scene.camera
     W, H, spp, depth = cam.image_width, cam.image_height, cam.samples_per_pixel, cam.max_depth
-    ctx = g.Context(local if world > 1 else 0)
+    ctx = g.Context(dev_index)
     ctx.set_blas_builder(args.blas)
     ctx.set_tlas_builder("reference" if args.blas == "reference" else "sah")
     ctx.upload(scene.desc)
@@ -130,7 +135,13 @@ def main():
             kernel_ms.append(ctx.last_render_kernel_ms())
             kernel_times.append(ctx.last_kernel_times())
         if dist is not None:
-            dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
+            if backend == "nccl":
+                dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)   # RCCL over xGMI
+            else:
+                host = accum.cpu()
+                dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+                if rank == 0:
+                    accum.copy_(host)
 
     # one HIP event before each extend/shade/shadow launch (and after each
     # shadow launch) on the render stream: per-kernel launch durations
@@ -148,7 +159,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -156,6 +167,9 @@ def main():
     value = samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
     img_ok = bool(torch.isfinite(accum).all().item()) if rank == 0 else True
+    # checksum of the combined frame: identical for any rank count (each pixel
+    # has one contributor and the RNG is keyed by global pixel id)
+    frame_sum = float(accum.double().sum().item()) if rank == 0 else None
 
     roofline = None
     work = None
@@ -227,7 +241,7 @@ def main():
                        "parallelism": f"tiles-rr{world}", "buckets": len(buckets), "blas": args.blas,
                        "triangles": info.triangles, "bvh_nodes": info.nodes,
                        "scene_build_s": round(t_build, 2), "device_bvh_build_ms": round(ctx.last_build_ms(), 2),
-                       "image_finite": img_ok},
+                       "image_finite": img_ok, "frame_sum": frame_sum},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -42,7 +42,10 @@
 #else
 #define RTG_WR_WORDS 9
 #endif
-#define RTG_TRAV_WAVES_FOR(kVol, kCount) (((kVol) || (kCount)) ? 4 : RTG_TRAV_WAVES)
+#ifndef RTG_VOL_WAVES
+#define RTG_VOL_WAVES 4
+#endif
+#define RTG_TRAV_WAVES_FOR(kVol, kCount) ((kCount) ? 4 : (kVol) ? RTG_VOL_WAVES : RTG_TRAV_WAVES)
 
 namespace rtg {
 
