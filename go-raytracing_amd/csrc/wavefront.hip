@@ -46,6 +46,11 @@
 #define RTG_VOL_WAVES 4
 #endif
 #define RTG_TRAV_WAVES_FOR(kVol, kCount) ((kCount) ? 4 : (kVol) ? RTG_VOL_WAVES : RTG_TRAV_WAVES)
+// any-hit shadow traversal carries no hit record: its own occupancy knob
+#ifndef RTG_SHADOW_WAVES
+#define RTG_SHADOW_WAVES RTG_TRAV_WAVES
+#endif
+#define RTG_SHADOW_WAVES_FOR(kVol, kCount) ((kCount) ? 4 : (kVol) ? RTG_VOL_WAVES : RTG_SHADOW_WAVES)
 
 namespace rtg {
 
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
 // contributions in that order, camera.go:549-558).  Lanes prefetch their next
 // job as k_extend does.
 template <int STACK, bool kCount, bool kVol, bool kEnvIS>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
+__global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[(STACK + RTG_WR_WORDS) * 256];   // stack ring + world ray
   if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
