@@ -165,6 +165,7 @@ def rtgpu() -> C.CDLL:
                                   C.POINTER(RtStats)]
         lib.rt_render_device.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams), P, P]
         lib.rt_last_render_kernel_ms.argtypes = [P, C.POINTER(C.c_double)]
+        lib.rt_sync.argtypes = [P]
         lib.rt_count_work.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
                                       C.POINTER(RtWorkCounts)]
         lib.rt_count_work_by_kernel.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
@@ -389,6 +390,10 @@ class Context:
     def render_device(self, camera: RtCameraDesc, params: RtRenderParams, dev_ptr: int, stream: int = 0):
         self._check(self._lib.rt_render_device(self._h, C.byref(camera), C.byref(params), C.c_void_p(dev_ptr),
                                                C.c_void_p(stream)))
+
+    def sync(self) -> None:
+        """Wait for every enqueued render; raises RTError(RT_ERR_DEVICE) on a device error."""
+        self._check(self._lib.rt_sync(self._h))
 
     def last_render_kernel_ms(self) -> float:
         ms = C.c_double()

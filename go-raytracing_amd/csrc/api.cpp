@@ -17,7 +17,7 @@
 #include "dev_layout.h"
 #include "build.h"
 #include "flatten.h"
-#include "render_launch.h"
+#include "probe.h"
 #include "wavefront.h"
 
 using namespace rtg;
@@ -38,10 +38,12 @@ struct rt_ctx {
   std::vector<DevBuf> scene_bufs;
   size_t scene_bytes = 0;
   // scratch
-  DevBuf partial, tiles, counters, errflag, accum, rgba, probe;
-  int4* tiles_pinned = nullptr;     // staging for async tile uploads
-  size_t tiles_pinned_n = 0;
-  hipEvent_t tiles_ev = nullptr;
+  DevBuf counters, errflag, accum, rgba, probe;
+  // errflag words: [0] sticky render flag (set by the traversal on a stack
+  // overflow, cleared only after the host has read it), [1] probe flag
+  int* err_pinned = nullptr;        // host copy of errflag[0], read by check_render_error
+  hipEvent_t err_ev = nullptr;      // after the copy of the latest render's flag
+  bool err_pending = false;         // a render's flag copy is in flight
   hipEvent_t kev0 = nullptr, kev1 = nullptr;   // render kernel only
   bool kev_recorded = false;
   // wavefront state
@@ -193,6 +195,30 @@ int make_tiles(rt_ctx* ctx, const rt_render_params* p, int W, int H, std::vector
   return RT_OK;
 }
 
+// Device errors of earlier renders (the traversal's stack-overflow flag,
+// device_common.h trav_step).  The flag word is sticky on the device: each
+// render enqueues an async copy of it to pinned memory; this reads that copy
+// once the copy has landed (wait: block until it has) and, if set, clears the
+// device word in stream order and reports RT_ERR_DEVICE.  rt_render_device
+// calls it without waiting on entry; every synchronising entry point
+// (rt_render, rt_sync, rt_last_render_kernel_ms, the count runs) waits.
+int check_render_error(rt_ctx* ctx, bool wait) {
+  if (!ctx->err_pending) return RT_OK;
+  if (wait) {
+    HIPCHK(hipEventSynchronize(ctx->err_ev));
+  } else {
+    const hipError_t q = hipEventQuery(ctx->err_ev);
+    if (q == hipErrorNotReady) return RT_OK;
+    if (q != hipSuccess) return hip_fail(ctx, q, "hipEventQuery(render error flag)");
+  }
+  ctx->err_pending = false;
+  if (*ctx->err_pinned == 0) return RT_OK;
+  *ctx->err_pinned = 0;
+  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow in a render (its frame is wrong)");
+}
+
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
 int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const std::vector<int4>& tiles, float* d_out,
@@ -241,7 +267,6 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->wacc, size_t(npix) * 3 * sizeof(double)))) return rc;
   if ((rc = ensure(ctx, ctx->counters, CNT_WORDS * sizeof(unsigned long long)))) return rc;
-  if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
   // pixel list through pinned staging (async-safe)
   HIPCHK(hipEventSynchronize(ctx->pix_ev));
   if (ctx->pix_pinned_n < npix) {
@@ -254,7 +279,6 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   std::memcpy(ctx->pix_pinned, px.data(), npix * sizeof(uint32_t));
   HIPCHK(hipMemcpyAsync(ctx->wpix.p, ctx->pix_pinned, npix * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(ctx->pix_ev, st));
-  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), st));
   if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
   WaveArgs a{};
   float4* base = static_cast<float4*>(ctx->wstate.p);
@@ -277,7 +301,12 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   a.max_depth = p->max_depth;
   a.counters = static_cast<unsigned long long*>(ctx->counters.p);
   a.err = static_cast<int*>(ctx->errflag.p);
-  static const int refill = [] { const char* e = getenv("RTGPU_REFILL"); return e ? std::max(1, atoi(e)) : 16; }();
+  // lanes that must want an item before a wave claims a new run (pool_take):
+  // within [1, 64] (the wave size), or no wave would ever claim
+  static const int refill = [] {
+    const char* e = getenv("RTGPU_REFILL");
+    return e ? std::min(64, std::max(1, atoi(e))) : 16;
+  }();
   a.refill = refill;
   WavePlan plan{};
   plan.spp = spp;
@@ -318,11 +347,13 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   HIPCHK(hipEventRecord(ctx->kev1, st));
   ctx->kev_recorded = true;
   if (ms) HIPCHK(hipEventRecord(ctx->ev1, st));
+  // the render's error flag follows it to the host asynchronously; it is
+  // read by the next entry point that synchronises (check_render_error)
+  HIPCHK(hipMemcpyAsync(ctx->err_pinned, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(ctx->err_ev, st));
+  ctx->err_pending = true;
   if (count || ms) {
-    HIPCHK(hipStreamSynchronize(st));
-    int flag = 0;
-    HIPCHK(hipMemcpy(&flag, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
+    if ((rc = check_render_error(ctx, true))) return rc;
     if (ms) {
       float f = 0.f;
       HIPCHK(hipEventElapsedTime(&f, ctx->ev0, ctx->ev1));
@@ -348,70 +379,7 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
   rc = make_tiles(ctx, p, dc.width, dc.height, tiles);
   if (rc) return rc;
   if (tiles.empty()) return RT_OK;
-  static const bool use_mega = [] { const char* e = getenv("RTGPU_PATH"); return e && std::string(e) == "mega"; }();
-  if (!use_mega) return render_wave(ctx, dc, p, tiles, d_out, st, count, host_counters, ms);
-  const int ntiles = int(tiles.size());
-  const int spp = p->samples_per_pixel;
-  // Enough workgroups to fill 256 CUs several times over; chunks of samples
-  // keep per-workgroup work bounded (tail) and results deterministic.
-  int chunks = std::max(1, std::min(spp, (16384 + ntiles - 1) / ntiles));
-  int chunk_spp = (spp + chunks - 1) / chunks;
-  chunks = (spp + chunk_spp - 1) / chunk_spp;
-  const size_t stride = size_t(ntiles) * 256 * 3;
-  if ((rc = ensure(ctx, ctx->tiles, tiles.size() * sizeof(int4)))) return rc;
-  if (!count && (rc = ensure(ctx, ctx->partial, size_t(chunks) * stride * sizeof(double)))) return rc;
-  if ((rc = ensure(ctx, ctx->counters, CNT_WORDS * sizeof(unsigned long long)))) return rc;
-  if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
-  // Stage through pinned memory; wait for the previous upload to finish reading it.
-  HIPCHK(hipEventSynchronize(ctx->tiles_ev));
-  if (ctx->tiles_pinned_n < tiles.size()) {
-    if (ctx->tiles_pinned) (void)hipHostFree(ctx->tiles_pinned);
-    ctx->tiles_pinned = nullptr;
-    ctx->tiles_pinned_n = 0;
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&ctx->tiles_pinned), tiles.size() * sizeof(int4)));
-    ctx->tiles_pinned_n = tiles.size();
-  }
-  std::memcpy(ctx->tiles_pinned, tiles.data(), tiles.size() * sizeof(int4));
-  HIPCHK(hipMemcpyAsync(ctx->tiles.p, ctx->tiles_pinned, tiles.size() * sizeof(int4), hipMemcpyHostToDevice, st));
-  HIPCHK(hipEventRecord(ctx->tiles_ev, st));
-  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), st));
-  if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
-  RenderLaunch w{};
-  w.tiles = static_cast<const int4*>(ctx->tiles.p);
-  w.ntiles = ntiles;
-  w.chunks = chunks;
-  w.chunk_spp = chunk_spp;
-  w.spp = spp;
-  w.max_depth = p->max_depth;
-  w.sample_offset = p->sample_offset;
-  w.seed = p->seed;
-  w.accumulate = p->accumulate ? 1 : 0;
-  w.partial = static_cast<double*>(ctx->partial.p);
-  w.partial_stride = stride;
-  w.counters = static_cast<unsigned long long*>(ctx->counters.p);
-  w.err = static_cast<int*>(ctx->errflag.p);
-  const int stack = ctx->host.stack_needed <= 32 ? 32 : 64;
-  if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
-  HIPCHK(hipEventRecord(ctx->kev0, st));
-  HIPCHK(launch_render(ctx->dscene, dc, w, stack, count, st));
-  HIPCHK(hipEventRecord(ctx->kev1, st));
-  ctx->kev_recorded = true;
-  if (!count) HIPCHK(launch_reduce(w, dc.width, d_out, st));
-  if (ms) HIPCHK(hipEventRecord(ctx->ev1, st));
-  if (count || ms) {
-    HIPCHK(hipStreamSynchronize(st));
-    int flag = 0;
-    HIPCHK(hipMemcpy(&flag, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
-    if (ms) {
-      float f = 0.f;
-      HIPCHK(hipEventElapsedTime(&f, ctx->ev0, ctx->ev1));
-      *ms = f;
-    }
-    if (count)
-      HIPCHK(hipMemcpy(host_counters, ctx->counters.p, CNT_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  }
-  return RT_OK;
+  return render_wave(ctx, dc, p, tiles, d_out, st, count, host_counters, ms);
 }
 
 }  // namespace
@@ -428,9 +396,13 @@ int rt_ctx_create(int device, rt_ctx** out) {
   if (device < 0 || device >= n) return RT_ERR_INVALID;
   rt_ctx* ctx = new rt_ctx();
   ctx->device = device;
+  ctx->errflag.bytes = 2 * sizeof(int);
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->tiles_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->err_ev, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->err_pinned), sizeof(int)) != hipSuccess ||
+      hipMalloc(&ctx->errflag.p, 2 * sizeof(int)) != hipSuccess ||
+      hipMemset(ctx->errflag.p, 0, 2 * sizeof(int)) != hipSuccess ||
       hipEventCreate(&ctx->kev0) != hipSuccess || hipEventCreate(&ctx->kev1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->pix_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&ctx->probe_pinned), 64) != hipSuccess ||
@@ -447,10 +419,10 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   free_scene(ctx);
-  free_buf(ctx->partial); free_buf(ctx->tiles); free_buf(ctx->counters); free_buf(ctx->errflag);
+  free_buf(ctx->counters); free_buf(ctx->errflag);
   free_buf(ctx->accum); free_buf(ctx->rgba); free_buf(ctx->probe);
-  if (ctx->tiles_pinned) (void)hipHostFree(ctx->tiles_pinned);
-  (void)hipEventDestroy(ctx->tiles_ev);
+  if (ctx->err_pinned) (void)hipHostFree(ctx->err_pinned);
+  if (ctx->err_ev) (void)hipEventDestroy(ctx->err_ev);
   free_buf(ctx->wstate); free_buf(ctx->wq); free_buf(ctx->wpix); free_buf(ctx->wacc);
   free_buf(ctx->wspill);
   if (ctx->pix_pinned) (void)hipHostFree(ctx->pix_pinned);
@@ -513,6 +485,8 @@ static int device_builds(rt_ctx* ctx) {
     if (e == hipSuccess) e = build_mesh_blas(job, static_cast<const DRefBox*>(boxes.p), tgt, res, ctx->stream);
     free_buf(boxes);
     if (e != hipSuccess) return hip_fail(ctx, e, "device BVH build");
+    if (uint64_t(tgt.nodes_used) + res.nodes_added >= kMaxNodes4)
+      return set_err(ctx, RT_ERR_UNSUPPORTED, "device-built BVH exceeds 32-bit BVH4 node offsets");
     tgt.nodes_used += res.nodes_added;
     tgt.leaves_used += res.leaves_added;
     ctx->dev_nodes += res.nodes_added;
@@ -672,7 +646,18 @@ int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_par
   if (!ctx || !cam || !accum_rgb_device) return RT_ERR_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+  // an earlier render's device error surfaces here at the latest (or at the
+  // next rt_sync / rt_last_render_kernel_ms)
+  int rc = check_render_error(ctx, false);
+  if (rc) return rc;
   return render_impl(ctx, cam, params, accum_rgb_device, st, false, nullptr, nullptr);
+}
+
+int rt_sync(rt_ctx* ctx) {
+  if (!ctx) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return check_render_error(ctx, true);
 }
 
 int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms) {
@@ -683,7 +668,7 @@ int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms) {
   float f = 0.f;
   HIPCHK(hipEventElapsedTime(&f, ctx->kev0, ctx->kev1));
   *ms = f;
-  return RT_OK;
+  return check_render_error(ctx, true);
 }
 
 namespace {
@@ -780,19 +765,19 @@ int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32
   if (rc) return rc;
   const size_t n = size_t(dc.width) * dc.height;
   if ((rc = ensure(ctx, ctx->probe, n * 12))) return rc;
-  if ((rc = ensure(ctx, ctx->errflag, sizeof(int)))) return rc;
   int32_t* top = static_cast<int32_t*>(ctx->probe.p);
   int32_t* prim = top + n;
   float* t = reinterpret_cast<float*>(prim + n);
-  HIPCHK(hipMemsetAsync(ctx->errflag.p, 0, sizeof(int), ctx->stream));
-  HIPCHK(launch_primary(ctx->dscene, dc, seed, sample, top, prim, t, static_cast<int*>(ctx->errflag.p),
+  int* perr = static_cast<int*>(ctx->errflag.p) + 1;   // the probe's own flag word
+  HIPCHK(hipMemsetAsync(perr, 0, sizeof(int), ctx->stream));
+  HIPCHK(launch_primary(ctx->dscene, dc, seed, sample, top, prim, t, perr,
                         ctx->host.stack_needed <= 32 ? 32 : 64, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   int flag = 0;
-  HIPCHK(hipMemcpy(&flag, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&flag, perr, sizeof(int), hipMemcpyDeviceToHost));
   if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
   return RT_OK;
 }

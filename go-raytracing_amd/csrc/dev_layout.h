@@ -84,6 +84,9 @@ struct alignas(16) DNode4 {
   uint32_t item[4];
   uint32_t pad[4];
 };
+// The traversal addresses nodes by 32-bit byte offset (index << 7): at most
+// 2^25 BVH4 nodes per scene (flatten / device_builds refuse more).
+constexpr uint32_t kMaxNodes4 = 1u << 25;
 
 struct alignas(8) DLeaf {
   uint32_t first;  // index into refs (PK_MIXED) or into the kind's prim array

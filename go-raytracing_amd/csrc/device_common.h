@@ -1,6 +1,18 @@
-// device_common.h — device-side building blocks shared by every kernel of
-// the path (render.hip megakernel/probe, wavefront.hip pipeline).  See the
-// file comment of render.hip for the reference functions restated here.
+// device_common.h — device-side building blocks shared by the kernels of the
+// path (wavefront.hip pipeline, probe.hip parity probe).  Reference functions
+// restated here (byvfx/go-raytracing rt/):
+//   GetRay                camera.go:368-434 (fast and slow path)
+//   BVHNode/BVHLeaf.Hit   bvh.go:26-37,219-239 (BVH4 while-while + DFS tie rule)
+//   AABB.Hit              aabb.go:59-116 (swap-on-negative slab, NaN keeps bounds)
+//   HittableList.Hit      hittable_list.go:31-45
+//   Sphere/Quad/Triangle/Plane/Circle.Hit  sphere.go:63-94 quad.go:44-84
+//                         triangle.go:57-104 plane.go:24-42 circle.go:37-72
+//   Translate/Rotate*/Scale.Hit  transform.go:93-106,159-191,229-272,310-353,408-444
+//   Volume.Hit            volume.go:34-79 (the BVH leaf wrapper tests it twice)
+//   Textures              texture.go:43-85, image_texture.go:26-41, noise.go
+//   HDRI Sample/PDF       hdri.go:75-128,228-322; PixelDataBilinear image_loader.go:398-436
+// The integrator itself (rayColorInternal camera.go:443-518, sampleLightMIS
+// :538-678, materials material.go:57-278) is k_shade in wavefront.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -85,6 +97,30 @@ __device__ __forceinline__ uint32_t ctr(uint32_t bounce, uint32_t dom, uint32_t 
 __device__ __forceinline__ float rnd(uint32_t key, uint32_t counter) {
   uint32_t h = lowbias32(key ^ lowbias32(counter ^ 0x632BE5ABu));
   return float(h >> 8) * 0x1p-24f;
+}
+
+// ln(x) for the volume free-flight -(1/rho)*ln(U) (volume.go:66), from
+// IEEE +,-,*,/ and bit operations only — no libm / ocml call — so the device
+// and the oracle's fp32 mode (oracle.c o_logf, the same algorithm) produce the
+// same bits and fog hits are bit-exact (ocml's and glibc's logf differ by an
+// ulp on some inputs).  x = m*2^e with m in [sqrt(1/2), sqrt(2)),
+// ln m = f - f^2/2 + s*(f^2/2 + R(s^2)) with f = m-1, s = f/(2+f) (fdlibm's
+// form, series to s^9), e*ln2 split hi/lo.
+// Within 2 ulp of ln over every RNG value k*2^-24 (tests/test_detlog.py);
+// x <= 0 gives -inf (U = 0: the free flight is infinite, as in Go).
+__device__ __forceinline__ float rt_logf(float x) {
+  if (!(x > 0.0f)) return -__builtin_inff();
+  const uint32_t b = __float_as_uint(x);
+  int e = int(b >> 23) - 127;
+  float m = __uint_as_float((b & 0x7FFFFFu) | 0x3F800000u);
+  if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+  const float f = m - 1.0f;                 // exact (Sterbenz)
+  const float hfsq = 0.5f * f * f;
+  const float s = f / (2.0f + f);
+  const float z = s * s;
+  const float R = z * (0.666666687f + z * (0.400000006f + z * (0.285714298f + z * 0.222222224f)));
+  const float fe = float(e);
+  return fe * 0.693145752f - ((hfsq - (s * (hfsq + R) + fe * 1.42860677e-06f)) - f);
 }
 
 // RandomUnitVector (vec3.go:45-54): rejection in the cube, 1e-160 < |p|^2 <= 1
@@ -398,7 +434,7 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
     float up = rnd(key, ctr(bounce, dom, uint32_t(vol.vol_id) * 4u + uint32_t(p)));
     u = up > u ? up : u;
   }
-  float hd = vol.neg_inv_density * logf(u);
+  float hd = vol.neg_inv_density * rt_logf(u);
   if (hd > dist) return false;
   t_out = t1 + hd / rl;
   return true;
@@ -735,9 +771,9 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
   V3 o = wo, d = wd;
   const DInstance* in = nullptr;
   if (b.inst >= 0) { in = &sc.instances[GIX(b.inst, sc.n_instances, 21)]; to_object(*in, o, d); }
-  rec.P = add(o, scale(d, b.t));
   // UVs (HitRecord.U/V) only when an ImageTexture needs them
   const bool uv = sc.needs_uv != 0;
+  if (b.kind != PK_TRI) rec.P = add(o, scale(d, b.t));
   if (b.kind == PK_SPHERE) {
     const DSphere& s = sc.spheres[GIX(b.idx, sc.n_spheres, 22)];
     V3 c = add(mk(s.cx, s.cy, s.cz), scale(mk(s.vx, s.vy, s.vz), time));
@@ -776,15 +812,22 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
     const DTriAux& ax = sc.tri_aux[GIX(b.idx, sc.n_tris, 24)];
     set_face(d, mk(ax.nx, ax.ny, ax.nz), rec);
     rec.mat = ax.mat;
-    if (uv) {                                     // triangle.go:57-101: Moller-Trumbore (u, v)
-      const DTri& tr = sc.tris[GIX(b.idx, sc.n_tris, 36)];
-      const V3 e1 = ld3(tr.e1), e2 = ld3(tr.e2);
-      const V3 h = cross(d, e2);
-      const float f = 1.0f / dot(e1, h);
-      const V3 sv = sub(o, ld3(tr.v0));
-      rec.u = f * dot(sv, h);
-      rec.v = f * dot(d, cross(sv, e1));
-    }
+    // Moller-Trumbore (u, v) of the winner (triangle.go:57-101).  The hit
+    // point is v0 + u*e1 + v*e2: equal to r.At(t) (triangle.go:97) to ~1e-13
+    // in the reference's float64, but in fp32 it lies on the triangle's plane
+    // where o + t*d can land up to an ulp of the ray's scale off it, and the
+    // next ray (tmin 0.001) then re-hits the surface it left: DESIGN.md §5
+    // (measured -0.24 % image-mean bias on CornellBoxLucy vs fp64, -0.02 %
+    // with this form).
+    const DTri& tr = sc.tris[GIX(b.idx, sc.n_tris, 36)];
+    const V3 v0 = ld3(tr.v0), e1 = ld3(tr.e1), e2 = ld3(tr.e2);
+    const V3 h = cross(d, e2);
+    const float f = 1.0f / dot(e1, h);
+    const V3 sv = sub(o, v0);
+    const float tu = f * dot(sv, h);
+    const float tv = f * dot(d, cross(sv, e1));
+    rec.P = add(v0, add(scale(e1, tu), scale(e2, tv)));
+    if (uv) { rec.u = tu; rec.v = tv; }
   }
   if (in) {
     for (int i = in->nwrap - 1; i >= 0; --i) unwrap_hit(in->kind[i], in->prm[i], rec.P, rec.N);
@@ -967,165 +1010,6 @@ __device__ __forceinline__ void get_ray(const DCamera& cam, int px, int py, uint
     ro = add(add(ro, scale(ld3(cam.disk_u), p.x)), scale(ld3(cam.disk_v), p.y));
   }
   rd = sub(ps, ro);
-}
-
-// ----------------------------------------------------------------------------
-// One camera sample (RayColor camera.go:438-518, iterative throughput form)
-// ----------------------------------------------------------------------------
-template <bool kCount>
-__device__ V3 trace_path(const DScene& sc, const DCamera& cam, int px, int py, uint32_t key, int depth,
-                         const TStack& S, Cnt& cnt, int* err) {
-  V3 ro, rd;
-  float time;
-  get_ray(cam, px, py, key, ro, rd, time);
-
-  V3 L = mk(0.0f, 0.0f, 0.0f), beta = mk(1.0f, 1.0f, 1.0f);
-  bool allow = true;
-  uint32_t bounce = 0;
-  for (int dleft = depth; dleft > 0; --dleft, ++bounce) {
-    Best b{};
-    if (kCount) cnt.rays++;
-    bool hit = traverse<false, kCount>(sc, ro, rd, time, 0.001f, __builtin_inff(), S, b, key,
-                                       bounce, DOM_VOL, cnt, err);
-    if (!hit) {                                               // camera.go:451-466
-      V3 bg;
-      if (sc.env.valid) {
-        if (cam.phantom && dleft == cam.cam_max_depth) bg = mk(0.0f, 0.0f, 0.0f);
-        else { bg = env_sample(sc.env, rd); if (kCount) cnt.env++; }
-      } else if (cam.use_sky) {
-        V3 ud = unit(rd);
-        float a = 0.5f * (ud.y + 1.0f);
-        bg = add(scale(mk(1.0f, 1.0f, 1.0f), 1.0f - a), scale(mk(0.5f, 0.7f, 1.0f), a));
-      } else {
-        bg = ld3(cam.background);
-      }
-      L = add(L, mul(beta, bg));
-      break;
-    }
-    Rec rec = make_record(sc, b, ro, rd, time);
-    const DMaterial& m = sc.materials[rec.mat];
-    if (kCount) cnt.mat++;
-    V3 att, sd;
-    bool use_mis = false;
-    if (m.kind == 4) {                                        // DiffuseLight: no scatter
-      if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.u, rec.v, rec.P)));
-      break;
-    } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
-      sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
-      if (near_zero(sd)) sd = rec.N;
-      att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
-      use_mis = sc.num_lights > 0;
-    } else if (m.kind == 2) {                                 // Metal material.go:113-119
-      V3 refl = reflect(rd, rec.N);
-      refl = add(unit(refl), scale(random_unit_vector(key, bounce, DOM_SCATTER, 0), m.fuzz));
-      sd = refl;
-      att = ld3(m.albedo);
-      if (!(dot(sd, rec.N) > 0.0f)) break;                    // absorbed: Emitted = 0
-    } else if (m.kind == 3) {                                 // Dielectric material.go:164-188
-      att = mk(1.0f, 1.0f, 1.0f);
-      float ri = rec.front ? (1.0f / m.ior) : m.ior;
-      V3 ud = unit(rd);
-      float c = dot(neg(ud), rec.N);
-      float ct = c < 1.0f ? c : 1.0f;
-      float st = sqrtf(1.0f - ct * ct);
-      bool cannot = ri * st > 1.0f;
-      bool refl = cannot;
-      if (!cannot) {
-        float r0 = (1.0f - ri) / (1.0f + ri);
-        r0 = r0 * r0;
-        float rf = r0 + (1.0f - r0) * pow5(1.0f - ct);
-        refl = rf > rnd(key, ctr(bounce, DOM_FRESNEL, 0));
-      }
-      sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
-    } else {                                                  // Isotropic material.go:266-270
-      sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
-      att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
-    }
-    if (use_mis) {                                            // camera.go:502-517
-      int nl = sc.num_lights;
-      int li = int(rnd(key, ctr(bounce, DOM_NEE, 0)) * float(nl));
-      if (li >= nl) li = nl - 1;
-      V3 direct = mk(0.0f, 0.0f, 0.0f);
-      if (sc.env.valid && sc.env.use_is) {                    // sampleHDRILight camera.go:565-607
-        const DEnv& e = sc.env;
-        V3 ldir, em;
-        float pdfH;
-        if (!(e.total_power > 0.0f)) {
-          ldir = random_unit_vector(key, bounce, DOM_NEE, 5);
-          em = env_sample(e, ldir);
-          pdfH = 1.0f / (4.0f * kPi);
-        } else {
-          float xi1 = rnd(key, ctr(bounce, DOM_NEE, 3));
-          int y = search_cdf(e.marginal, e.height, xi1);
-          float xi2 = rnd(key, ctr(bounce, DOM_NEE, 4));
-          int x = search_cdf(e.conditional + size_t(y) * (e.width + 1), e.width, xi2);
-          float uu = (float(x) + 0.5f) / float(e.width);
-          float vv = (float(y) + 0.5f) / float(e.height);
-          uu = uu - e.rotation / (2.0f * kPi);               // UVToDirection hdri.go:97-113
-          uu = uu - floorf(uu);
-          float phi = (uu - 0.5f) * 2.0f * kPi;
-          float th = (0.5f - vv) * kPi;
-          float ctt = cosf(th);
-          ldir = mk(ctt * cosf(phi), sinf(th), ctt * sinf(phi));
-          em = texel(e, x, y);
-          pdfH = env_pdf(e, ldir);
-        }
-        float cth = dot(rec.N, ldir);
-        if (cth > 0.0f) {
-          Best sb{};
-          if (kCount) cnt.shadow++;
-          bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, __builtin_inff(), S,
-                                                sb, key, bounce, DOM_VOL_SH_HDRI, cnt, err);
-          if (!blocked) {
-            float c2 = dot(rec.N, ldir);
-            float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
-            float w = pdfH / (pdfH + pdfB);
-            V3 ct = mul(scale(em, cth / pdfH * w), att);
-            direct = add(direct, mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f)));
-          }
-        }
-      }
-      if (li < nl) {                                          // sampleAreaLight camera.go:610-678
-        const DLight& lt = sc.lights[li];
-        if (lt.is_quad) {
-          float al = rnd(key, ctr(bounce, DOM_NEE, 1)), be = rnd(key, ctr(bounce, DOM_NEE, 2));
-          V3 lp = add(add(ld3(lt.Q), scale(ld3(lt.u), al)), scale(ld3(lt.v), be));
-          V3 tl = sub(lp, rec.P);
-          float dist = len(tl);
-          V3 ldir = unit(tl);
-          float cth = dot(rec.N, ldir);
-          if (cth > 0.0f) {
-            Best sb{};
-            if (kCount) cnt.shadow++;
-            bool blocked = traverse<true, kCount>(sc, rec.P, ldir, 0.0f, 0.001f, dist - 0.001f, S,
-                                                  sb, key, bounce, DOM_VOL_SH_AREA, cnt, err);
-            if (!blocked) {
-              const DMaterial& lm = sc.materials[lt.mat];
-              V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
-              float area = len(cross(ld3(lt.u), ld3(lt.v)));
-              float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
-              if (!(cl < 0.001f)) {
-                float pdfL = (dist * dist) / (cl * area);
-                float c2 = dot(rec.N, ldir);
-                float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
-                float w = pdfL / (pdfL + pdfB);
-                V3 ct = scale(mul(scale(em, cth / pdfL * w), att), float(nl));
-                direct = add(direct, mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f)));
-              }
-            }
-          }
-        }
-      }
-      L = add(L, mul(beta, direct));
-      allow = false;
-    } else {
-      allow = true;
-    }
-    beta = mul(beta, att);
-    ro = rec.P;
-    rd = sd;
-  }
-  return L;
 }
 
 }  // namespace rtg

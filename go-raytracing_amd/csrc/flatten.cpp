@@ -553,8 +553,14 @@ struct Flattener {
       if (!valid_index(h.a)) return fail(RT_ERR_INVALID, "bad volume boundary");
       int inst = make_instance(h.a);
       if (inst < 0) return false;
-      const DBvh& bb = S.blas[S.instances[inst].blas];
-      if ((bb.root_item >> ITEM_SHIFT) != ITEM_LEAF)
+      const int bl = S.instances[inst].blas;
+      const DBvh& bb = S.blas[bl];
+      // (a boundary queued for the device builder holds a placeholder leaf
+      // root here; it becomes a node root at upload, which volume_hit cannot
+      // walk: the same refusal as a host-built BVH boundary)
+      bool device_built = false;
+      for (const auto& j : S.device_builds) device_built = device_built || j.blas == bl;
+      if ((bb.root_item >> ITEM_SHIFT) != ITEM_LEAF || device_built)
         return fail(RT_ERR_UNSUPPORTED, "volume boundary must be a list/primitive (not a BVH)");
       DVolume v{};
       v.boundary = inst;
@@ -1110,6 +1116,12 @@ struct Flattener {
     if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
     if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27) || S.nodes4.size() >= (1u << 27))
       fail(RT_ERR_UNSUPPORTED, "scene too large for 28-bit indices");
+    // BVH4 node addresses are 32-bit byte offsets (index << 7, trav_step):
+    // host nodes plus the device builder's room (< n nodes per queued mesh)
+    // must stay below kMaxNodes4
+    size_t dev_room = 0;
+    for (const auto& j : S.device_builds) dev_room += j.n;
+    if (S.nodes4.size() + dev_room >= kMaxNodes4) fail(RT_ERR_UNSUPPORTED, "scene too large for 32-bit BVH4 node offsets");
     return status;
   }
 };

@@ -780,6 +780,35 @@ static Scene cornell_smoke() {   // scenes.go:820-925
   return s;
 }
 
+// Test-only variant (RotateX/RotateZ parity): the Cornell room
+// with boxes, a pyramid and a sphere under RotateX / RotateZ wrappers built by
+// Transform.Apply (Scale -> RotX -> RotY -> RotZ -> Translate,
+// transform.go:24-46).  RotateX/RotateZ rotate the ray the same way as their
+// bbox (transform.go:201-353, "as written"), so the objects Hit sees are not
+// inside the bboxes the world BVH culls with; the reference clips them there
+// and so must the device (it keeps the caller's world topology for them).
+static Scene cornell_rotations() {
+  Scene s;
+  s.world = NewHittableList();
+  auto white = NewLambertian({0.73, 0.73, 0.73});
+  auto red = NewLambertian({0.65, 0.05, 0.05});
+  auto green = NewLambertian({0.12, 0.45, 0.15});
+  auto light = NewDiffuseLight(NewSolidColor({15, 15, 15}));
+  auto area = cornell_walls(*s.world, white, red, green, light);
+  auto blue = NewLambertian({0.2, 0.3, 0.8});
+  s.world->Add(Transform().SetRotation({30, 0, 0}).SetPosition({120, 80, 220}).Apply(Box({0, 0, 0}, {140, 200, 120}, white)));
+  s.world->Add(Transform().SetRotation({0, 0, -25}).SetPosition({360, 40, 300}).Apply(Box({0, 0, 0}, {120, 160, 120}, blue)));
+  s.world->Add(Transform().SetScale({1.2, 0.8, 1.0}).SetRotation({15, 40, -10}).SetPosition({280, 260, 150})
+                   .Apply(Box({0, 0, 0}, {90, 90, 90}, red)));
+  s.world->Add(Transform().SetRotation({-20, 0, 35}).SetPosition({170, 330, 380}).Apply(Pyramid({0, 0, 0}, 110, 130, green)));
+  s.world->Add(Transform().SetRotation({0, 0, 50}).SetPosition({430, 300, 200}).Apply(NewSphere({40, 0, 0}, 55, white)));
+  s.world->Add(Transform().SetRotation({70, 0, 0}).SetPosition({300, 420, 420}).Apply(NewSphere({0, 0, -30}, 40, blue)));
+  s.camera = std::make_shared<Camera>();
+  s.camera->SetResolution(600, 1.0).SetQuality(50, 5).SetPosition({278, 278, -800}, {278, 278, 0}, {0, 1, 0})
+      .SetLens(40, 0, 10).SetBackground({0, 0, 0}).AddLight(area).Build();
+  return s;
+}
+
 static bool file_exists(const std::string& p) { struct stat st; return ::stat(p.c_str(), &st) == 0; }
 
 static bool cornell_lucy(const SceneOptions& o, Scene& s, std::string& err) {   // scenes.go:714-817
@@ -969,6 +998,7 @@ bool MakeScene(const std::string& name, const SceneOptions& opt, Scene& out, std
   else if (name == "random") out = random_scene(opt.seed);
   else if (name == "cornell") out = cornell_scene();
   else if (name == "cornell-smoke") out = cornell_smoke();
+  else if (name == "cornell-rotations") out = cornell_rotations();
   else if (name == "cornell-lucy") { if (!cornell_lucy(opt, out, err)) return false; }
   else if (name == "hdri-test") { if (!hdri_scene(opt, out, err, false)) return false; }
   else if (name == "hdri-nee") { if (!hdri_scene(opt, out, err, true)) return false; }

@@ -1,0 +1,13 @@
+// probe.h — host-side launch interface of probe.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dev_layout.h"
+
+namespace rtg {
+
+hipError_t launch_tonemap(const float* accum, int n, int spp, uint8_t* rgba, hipStream_t st);
+hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, int sample, int32_t* top,
+                          int32_t* prim, float* t, int* err, int stack, hipStream_t st);
+
+}  // namespace rtg

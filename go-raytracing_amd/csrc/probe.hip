@@ -1,0 +1,93 @@
+// probe.hip — the small kernels beside the wavefront pipeline
+// (wavefront.hip, the render path):
+//   * tonemap_kernel: the reference's RGBA8 quantisation of a pass
+//     (bucket_renderer.go:276-285, utils.go:85-90) for rt_tonemap_rgba8;
+//   * primary_kernel: the parity probe rt_primary_hits — one sample's
+//     GetRay (camera.go:368-434) + closest hit (world.Hit, camera.go:449)
+//     per pixel, through the same traversal as k_extend (device_common.h
+//     traverse / trav_step), reporting the hit hittable ids and t.
+// Arithmetic is fp32 in the Go operation order (-ffp-contract=off), which the
+// CPU oracle's fp32 mode reproduces.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dev_layout.h"
+#include "device_common.h"
+#include "probe.h"
+
+namespace rtg {
+
+// ----------------------------------------------------------------------------
+// Kernels
+// ----------------------------------------------------------------------------
+// bucket_renderer.go:276-285: scale 1/spp, LinearToGamma (utils.go:85-90),
+// clamp [0,0.999], uint8(256*x) — in fp64 like the reference.
+__global__ void tonemap_kernel(const float* accum, int n, int spp, uint8_t* rgba) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double sc = 1.0 / double(spp);
+  uint8_t o[4];
+  for (int c = 0; c < 3; ++c) {
+    double v = double(accum[size_t(i) * 3 + c]) * sc;
+    double g = v > 0.0 ? sqrt(v) : 0.0;
+    if (g < 0.0) g = 0.0;
+    if (g > 0.999) g = 0.999;
+    o[c] = uint8_t(256.0 * g);
+  }
+  o[3] = 255;
+  reinterpret_cast<uchar4*>(rgba)[i] = make_uchar4(o[0], o[1], o[2], o[3]);
+}
+
+// Parity probe: first-bounce closest hit of one sample per pixel.
+template <int STACK>
+__global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, uint32_t seed, int sample,
+                                                      int32_t* out_top, int32_t* out_prim, float* out_t, int* err) {
+  __shared__ uint32_t lds_stack[(STACK + 9) * 256];   // stack + world ray
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x * 256 + tid;
+  if (i >= cam.width * cam.height) return;
+  const int px = i % cam.width, py = i / cam.width;
+  uint32_t key = path_key(seed, uint32_t(i), uint32_t(sample));
+  V3 ro, rd;
+  float time;
+  get_ray(cam, px, py, key, ro, rd, time);
+  Best b{};
+  Cnt cnt = {};
+  bool hit = traverse<false, false>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack_only(lds_stack + tid, 256, STACK), b, key,
+                                    0, DOM_VOL, cnt, err);
+  int top = -1, prim = -1;
+  if (hit) {
+    if (b.kind == PK_PLANE) { top = prim = sc.plane_hidx[b.idx]; }
+    else {
+      top = sc.tlas_ref_top[b.refpos];
+      if (b.kind == PK_SPHERE) prim = sc.sphere_hidx[b.idx];
+      else if (b.kind == PK_QUAD) prim = sc.quad_hidx[b.idx];
+      else if (b.kind == PK_TRI) prim = sc.tri_hidx[b.idx];
+      else if (b.kind == PK_CIRCLE) prim = sc.circle_hidx[b.idx];
+      else prim = sc.volume_hidx[b.idx];
+    }
+  }
+  out_top[i] = top;
+  out_prim[i] = prim;
+  out_t[i] = hit ? b.t : -1.0f;
+}
+
+// ----------------------------------------------------------------------------
+// Host launchers
+// ----------------------------------------------------------------------------
+hipError_t launch_tonemap(const float* accum, int n, int spp, uint8_t* rgba, hipStream_t st) {
+  hipLaunchKernelGGL(tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, st, accum, n, spp, rgba);
+  return hipGetLastError();
+}
+
+hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, int sample, int32_t* top,
+                          int32_t* prim, float* t, int* err, int stack, hipStream_t st) {
+  int n = cam.width * cam.height;
+  dim3 grid((n + 255) / 256), block(256);
+  if (stack <= 32)
+    hipLaunchKernelGGL((primary_kernel<32>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+  else
+    hipLaunchKernelGGL((primary_kernel<64>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+  return hipGetLastError();
+}
+
+}  // namespace rtg

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -277,13 +277,22 @@ int rt_render(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* pa
               float* accum_rgb, rt_stats* stats);
 
 /* Same, into a device buffer (width*height*3 float) on `hip_stream`;
- * asynchronous.  Used by the multi-GPU driver (tile shard + RCCL combine). */
+ * asynchronous.  Used by the multi-GPU driver (tile shard + RCCL combine).
+ * A device-side error of a render (RT_ERR_DEVICE: traversal stack overflow,
+ * the frame is wrong) is reported by the first of: the next rt_render_device
+ * call once that render has finished, rt_sync, rt_last_render_kernel_ms.   */
 int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                      float* accum_rgb_device, void* hip_stream);
 
+/* Blocks until every render enqueued on this context has finished and
+ * reports any device-side error of them (RT_ERR_DEVICE), as the Go
+ * renderer's pass completion (bucket_renderer.go:212-213, wg.Wait) would.  */
+int rt_sync(rt_ctx* ctx);
+
 /* Device time (ms) of the render kernel of the most recent render call on
  * this context (hipEvents recorded on that call's stream around the render
- * kernel only); blocks until that kernel has finished.                    */
+ * kernel only); blocks until that kernel has finished and reports a device
+ * error of the renders so far (RT_ERR_DEVICE).                             */
 int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms);
 
 /* Instrumented run of the same kernel: traversal/prim counters. */

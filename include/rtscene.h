@@ -39,7 +39,8 @@ typedef struct rts_scene rts_scene;
 /* name: "simple" | "random" | "cornell" | "cornell-lucy" | "hdri-test" |
  *       "cornell-smoke" | "quads" | "primitives" | "perlin" | "earth" |
  *       "checkered-spheres" | "glossy-metal" | "cornell-glossy" |
- *       "hdri-nee" (test-only: HDRI + quad light).
+ *       "hdri-nee" (test-only: HDRI + quad light),
+ *       "cornell-rotations" (test-only: RotateX / RotateZ wrappers).
  * The world is wrapped in NewBVHNodeFromList like main.go:77.            */
 int rts_scene_create(const char* name, const rts_scene_options* opt, rts_scene** out, char* err, int32_t errlen);
 void rts_scene_destroy(rts_scene* s);

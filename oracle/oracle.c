@@ -161,6 +161,7 @@ static void oscene_free(OScene* os) {
 #define UNITVEC_LO 1e-160
 #define BOX_LO(x) (x)
 #define BOX_HI(x) (x)
+#define TRI_P_BARY 0
 #include "oracle_impl.h"
 #undef REAL
 #undef SUF
@@ -178,9 +179,35 @@ static void oscene_free(OScene* os) {
 #undef UNITVEC_LO
 #undef BOX_LO
 #undef BOX_HI
+#undef TRI_P_BARY
 
 /* ------------------------------------------------------------ fp32 instantiation */
 static inline float o_pow5f(float x) { float x2 = x * x; return (x2 * x2) * x; }
+/* ln(x) of the volume free flight (volume.go:66) in fp32 mode: the device's
+ * libm-free algorithm (device_common.h rt_logf), restated so both sides give
+ * the same bits: x = m*2^e, m in [sqrt(1/2), sqrt(2)),
+ * ln m = f - f^2/2 + s*(f^2/2 + R(s^2)), f = m-1, s = f/(2+f) (fdlibm's form,
+ * series to s^9), e*ln2 split hi/lo.  x <= 0 -> -inf. */
+static inline float o_logf(float x) {
+  if (!(x > 0.0f)) return -INFINITY;
+  uint32_t b;
+  memcpy(&b, &x, 4);
+  int e = (int)(b >> 23) - 127;
+  uint32_t mb = (b & 0x7FFFFFu) | 0x3F800000u;
+  float m;
+  memcpy(&m, &mb, 4);
+  if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+  const float f = m - 1.0f;
+  const float hfsq = 0.5f * f * f;
+  const float s = f / (2.0f + f);
+  const float z = s * s;
+  const float R = z * (0.666666687f + z * (0.400000006f + z * (0.285714298f + z * 0.222222224f)));
+  const float fe = (float)e;
+  return fe * 0.693145752f - ((hfsq - (s * (hfsq + R) + fe * 1.42860677e-06f)) - f);
+}
+void oracle_logf32(const float* in, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = o_logf(in[i]);
+}
 static inline float o_round_down(double x) {
   float f = (float)x;
   if (isfinite(x) && (double)f > x) f = nextafterf(f, -INFINITY);
@@ -195,7 +222,7 @@ static inline float o_round_up(double x) {
 #define SUF _f
 #define SQRT sqrtf
 #define FABS fabsf
-#define LOG logf
+#define LOG o_logf
 #define COS cosf
 #define SIN sinf
 #define ATAN2 atan2f
@@ -207,6 +234,7 @@ static inline float o_round_up(double x) {
 #define UNITVEC_LO 0.0f
 #define BOX_LO(x) o_round_down(x)
 #define BOX_HI(x) o_round_up(x)
+#define TRI_P_BARY 1
 #include "oracle_impl.h"
 
 /* ------------------------------------------------------------ public API */

@@ -44,6 +44,7 @@ void oracle_tonemap(const float* accum, int64_t npix, int32_t spp, uint8_t* rgba
 
 /* RNG known-answer hook: uniform (24-bit) for (seed, pixel, sample, counter). */
 double oracle_rng_uniform(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t counter);
+void oracle_logf32(const float* in, float* out, int64_t n);
 
 /* NewBVHNode (bvh.go:69-217) over n boxes {xmin,xmax,ymin,ymax,zmin,zmax}.
  * Output: preorder encoding, internal node = -1, leaf = count followed by

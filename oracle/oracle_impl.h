@@ -256,7 +256,10 @@ static int FN(tri_hit)(FN(TC)* c, int g, FN(Ray) r, REAL mn, REAL mx, FN(Rec)* r
   REAL t = f * FN(dot)(e2, q);
   if (!(mn <= t && t <= mx)) return 0;
   rec->t = t;
-  rec->P = FN(at)(r, t);
+  /* triangle.go:97 r.At(t); the fp32 mode takes v0 + u*e1 + v*e2 like the
+   * device (make_record), which removes fp32's self-intersection bias
+   * (DESIGN.md §5); in float64 the two agree to ~1e-13. */
+  rec->P = TRI_P_BARY ? FN(add)(v0, FN(add)(FN(scale)(e1, u), FN(scale)(e2, v))) : FN(at)(r, t);
   rec->u = u;                                                    /* triangle.go:100-101 */
   rec->v = v;
   rec->mat = c->S->os->d->hittables[g].material;

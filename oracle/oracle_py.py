@@ -35,6 +35,8 @@ def lib():
         L.oracle_tonemap.restype = None
         L.oracle_rng_uniform.argtypes = [C.c_uint32] * 4
         L.oracle_rng_uniform.restype = C.c_double
+        L.oracle_logf32.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int64]
+        L.oracle_logf32.restype = None
         L.oracle_build_bvh.argtypes = [C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int32), C.c_int32]
         L.oracle_load_hdr.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_double), C.c_int64]

@@ -1,0 +1,68 @@
+"""C-ABI behaviour on the GPU beyond parity (rtgpu.h): the asynchronous
+rt_render_device path and its error reporting, and scene refusals.  Marked gpu."""
+import numpy as np
+import pytest
+
+from tests.scene_builder import Builder
+
+pytestmark = pytest.mark.gpu
+
+
+def test_render_device_equals_render_and_sync(g, ctx):
+    """rt_render_device (the bench / multi-GPU path) renders the same frame as
+    rt_render; rt_sync waits for it and reports no device error."""
+    import torch
+    s = g.Scene("cornell", width=64)
+    cam = s.camera
+    ctx.upload(s.desc)
+    p = g.make_params(4, 5, seed=21)
+    host, _ = ctx.render(cam, p)
+    buf = torch.zeros(cam.image_height * cam.image_width * 3, dtype=torch.float32, device="cuda:0")
+    stream = torch.cuda.current_stream()
+    for _ in range(3):   # several renders in flight before the check
+        buf.zero_()
+        ctx.render_device(cam, p, buf.data_ptr(), stream.cuda_stream)
+    ctx.sync()
+    assert ctx.last_render_kernel_ms() > 0.0
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy().reshape(host.shape), host)
+
+
+def _mesh_bvh(g, b, tris):
+    """A BVHNode tree over triangles: median split, leaves of <= 4 wrapped as
+    BVHNode{leaf, leaf} (bvh.go:120-217 shape)."""
+    if len(tris) <= 4:
+        return b.leaf_node(tris)
+    m = len(tris) // 2
+    lo, hi = _mesh_bvh(g, b, tris[:m]), _mesh_bvh(g, b, tris[m:])
+    bb = [min(b.h[lo].bbox[0], b.h[hi].bbox[0]), max(b.h[lo].bbox[1], b.h[hi].bbox[1]),
+          min(b.h[lo].bbox[2], b.h[hi].bbox[2]), max(b.h[lo].bbox[3], b.h[hi].bbox[3]),
+          min(b.h[lo].bbox[4], b.h[hi].bbox[4]), max(b.h[lo].bbox[5], b.h[hi].bbox[5])]
+    return b._add(g.RT_BVH_NODE, -1, lo, hi, bb, [])
+
+
+@pytest.mark.parametrize("builder", ["reference", "sah", "device"])
+def test_volume_with_mesh_boundary_refused(g, builder):
+    """Volume.Hit over a BVH boundary is outside the device path: every BLAS
+    builder refuses it with RT_ERR_UNSUPPORTED (the Go caller keeps its CPU
+    renderer), including the device builder, whose placeholder root used to
+    slip past the check."""
+    b = Builder(g)
+    m = b.lambertian((0.5, 0.5, 0.5))
+    tris = []
+    for i in range(12):           # a closed-ish fan of 48 triangles
+        for k in range(4):
+            x = float(i)
+            tris.append(b.triangle((x, 0, k), (x + 1, 0, k), (x, 1, k + 0.5), m))
+    mesh = _mesh_bvh(g, b, tris)
+    iso = b.mat(g.RT_ISOTROPIC, b.solid((1, 1, 1)))
+    vol = b.volume(mesh, 0.1, iso)
+    root = b.listing([vol, b.sphere((0, 0, -5), 1.0, m)])
+    c = g.Context(0)
+    try:
+        c.set_blas_builder(builder)
+        with pytest.raises(g.RTError) as ei:
+            c.upload(b.desc(root))
+        assert ei.value.code == -2, str(ei.value)
+    finally:
+        c.close()

@@ -1,10 +1,15 @@
 """GPU (HIP, via the C-ABI) vs CPU oracle parity.  Marked gpu.
 
 Tolerances (stated, BASELINE.json north_star):
-  * first-bounce closest-hit ids (top-level object, primitive): bit-exact vs the
-    oracle's fp32 mirror mode;
-  * radiance: image mean over pixels of the squared RGB error of the per-pixel
-    average radiance < 1e-4 vs the fp32 oracle (same counter RNG keys);
+  * first-bounce closest-hit ids (top-level object, primitive) and hit t:
+    bit-exact vs the oracle's fp32 mirror mode, every scene (fog included: the
+    free-flight log is libm-free on both sides, tests/test_detlog.py);
+  * radiance vs the fp32 mirror: image mean over pixels of the squared RGB
+    error of the per-pixel average radiance < 1e-4 (same counter RNG keys);
+  * radiance vs the oracle's float64 mode (the Go arithmetic, camera.go:443-518
+    in float64) on the BASELINE configs: the same image-mean squared error
+    <= 1e-4 at the spp stated per config in FP64_CASES, and the image-mean
+    relative bias within 2e-3;
   * RGBA8 quantisation: bit-exact given the same float sums.
 """
 import numpy as np
@@ -28,6 +33,7 @@ SCENES = [
     ("checkered-spheres", dict(width=96)),
     ("glossy-metal", dict(width=96)),
     ("cornell-glossy", dict(width=64)),
+    ("cornell-rotations", dict(width=64)),
 ]
 
 
@@ -44,14 +50,9 @@ def test_primary_hits_bit_exact(g, O, ctx, name, kw):
         tg, pg, t_g = ctx.primary_hits(cam, 1234, sample)
         to, po, t_o = O.primary_hits(s.desc, cam, 1234, sample, fp32=True)
         mism = np.flatnonzero((tg != to) | (pg != po))
-        # volumes draw log(U): libm vs ocml may differ by an ulp -> allow a
-        # vanishing fraction only for scenes with fog.
-        allowed = 0 if "cornell" not in name or name == "cornell-lucy" else max(1, tg.size // 2000)
-        assert mism.size <= allowed, f"{name}: {mism.size} mismatches, first {mism[:5]}"
-        same = (tg == to) & (pg == po) & (tg >= 0)
-        if name in ("simple", "random", "cornell-lucy", "hdri-test", "hdri-nee", "quads", "primitives", "perlin",
-                    "earth", "checkered-spheres", "glossy-metal", "cornell-glossy"):
-            assert np.array_equal(t_g[same], t_o[same].astype(np.float32)), f"{name}: hit t differs"
+        assert mism.size == 0, f"{name}: {mism.size} mismatches, first {mism[:5]}"
+        hit = tg >= 0
+        assert np.array_equal(t_g[hit], t_o[hit].astype(np.float32)), f"{name}: hit t differs"
         assert (tg >= 0).any()
 
 
@@ -70,12 +71,9 @@ def test_bvh_builders_same_hits(g, O, builder, name):
         c.upload(s.desc)
         tg, pg, t_g = c.primary_hits(cam, 99, 1)
         to, po, t_o = O.primary_hits(s.desc, cam, 99, 1, fp32=True)
-        mism = np.flatnonzero((tg != to) | (pg != po))
-        allowed = max(1, tg.size // 2000) if name == "cornell-smoke" else 0   # fog: log(U) libm ulps
-        assert mism.size <= allowed, f"{mism.size} mismatches"
-        hit = (tg >= 0) & (tg == to) & (pg == po)
-        if name != "cornell-smoke":
-            assert np.array_equal(t_g[hit], t_o[hit].astype(np.float32))
+        assert np.array_equal(tg, to) and np.array_equal(pg, po)
+        hit = tg >= 0
+        assert np.array_equal(t_g[hit], t_o[hit].astype(np.float32))
     finally:
         c.close()
 
@@ -95,20 +93,42 @@ def test_radiance_parity_fp32(g, O, ctx, name, kw):
     assert gpu.mean() > 0
 
 
-@pytest.mark.parametrize("name,kw", SCENES[:3], ids=[s[0] for s in SCENES[:3]])
-def test_radiance_vs_fp64_reference(g, O, ctx, name, kw):
-    """fp32 GPU vs the fp64 restatement of the Go arithmetic: statistical."""
+# BASELINE configs (C1 SimpleScene, C2 RandomScene, C3 CornellBoxScene, C4
+# CornellBoxLucy with the full 280K-triangle mesh, C5 HDRITestScene) at reduced
+# resolution, plus the fog and RotateX/Z variants: (scene, kwargs, spp).  The
+# fp32-vs-float64 error is dominated by paths whose branch (a dielectric
+# reflect/refract draw, a grazing hit, a rejection-sampling loop) flips between
+# the two precisions; it falls as 1/spp.  HDRITestScene needs 128 spp: its
+# flipped paths carry HDRI radiance up to 77.75 (measured 5.7e-4 at 16 spp,
+# 3e-5..7e-5 at 64, 1.8e-5..3.9e-5 at 128 over seeds 5-7).
+FP64_CASES = [
+    ("simple", dict(width=96), 64),
+    ("random", dict(width=96), 64),
+    ("cornell", dict(width=64), 64),
+    ("cornell-smoke", dict(width=64), 64),
+    ("cornell-lucy", dict(width=64), 64),
+    ("hdri-test", dict(width=96), 128),
+    ("cornell-rotations", dict(width=64), 64),
+]
+
+
+@pytest.mark.parametrize("name,kw,spp", FP64_CASES, ids=[c[0] for c in FP64_CASES])
+def test_radiance_vs_fp64_reference(g, O, ctx, name, kw, spp):
+    """fp32 GPU vs the float64 restatement of the Go arithmetic, same RNG keys:
+    per-pixel L2 <= 1e-4 (image mean) and image-mean relative bias <= 2e-3."""
     s = _scene(g, name, kw)
     cam = s.camera
-    spp = 16
     ctx.upload(s.desc)
     p = g.make_params(spp, cam.max_depth, seed=5)
     gpu, _ = ctx.render(cam, p)
-    ref = O.render(s.desc, cam, p, fp32=False)
+    ref = O.render(s.desc, cam, p, fp32=False, threads=16)
     a = gpu.astype(np.float64) / spp
     b = ref / spp
-    assert abs(a.mean() - b.mean()) < 0.02 * max(b.mean(), 1e-3)
-    assert float(np.mean((a - b) ** 2)) < 1e-2
+    mse = float(np.mean((a - b) ** 2))
+    bias = float((a.mean() - b.mean()) / max(b.mean(), 1e-6))
+    print(f"fp64 tolerance {name} {cam.image_width}x{cam.image_height} {spp}spp: mse {mse:.3e} rel_bias {bias:+.2e}")
+    assert mse <= 1e-4, f"{name}: mse {mse:.3e}"
+    assert abs(bias) <= 2e-3, f"{name}: relative bias {bias:+.3e}"
 
 
 def test_tonemap_bit_exact(g, O, ctx):
@@ -166,17 +186,40 @@ def test_count_work(g, ctx):
     assert w["shadow_rays"] > 0
 
 
-def test_bucket_renderer_three_passes(g, tmp_path):
-    s = g.Scene("cornell", width=64, spp=8)
-    r = g.BucketRenderer(s, 32, 8, 0, seed=1)
+@pytest.mark.parametrize("name", ["cornell", "hdri-test"])
+def test_bucket_renderer_three_passes(g, O, tmp_path, name):
+    """The progressive 3-pass schedule (bucket_renderer.go:175-191): pass k
+    renders (1 spp, depth 3), (max(1, spp/4), max(3, depth/2)), (spp, depth)
+    and OVERWRITES the framebuffer (renderBucketWithQuality :257-301).  Each
+    pass's accumulation matches the oracle's render of that pass's
+    spp/depth/seed over the centre-out buckets, its RGBA8 framebuffer is the
+    reference quantisation (:276-285) of that accumulation, bit for bit, and
+    SaveImage's PNG decodes back to the final framebuffer."""
+    from tests.pngdec import read_png
+    s = g.Scene(name, width=64, spp=8)
+    cam = s.camera
+    seed = 1
+    r = g.BucketRenderer(s, 32, 8, 0, seed=seed)
     assert not r.is_completed()
-    r.render_all()
-    assert r.is_completed()
-    fb = r.framebuffer()
-    assert fb.shape == (64, 64, 4) and (fb[..., 3] == 255).all() and fb[..., :3].max() > 0
+    spp_full, depth_full = cam.samples_per_pixel, cam.max_depth
+    schedule = [(1, 3), (max(1, spp_full // 4), max(3, depth_full // 2)), (spp_full, depth_full)]
+    buckets = g.generate_buckets(cam.image_width, cam.image_height, 32)
+    for k, (spp, depth) in enumerate(schedule):
+        r.render_pass(k)
+        assert r.is_completed() == (k == 2)
+        acc, fb = r.accum(), r.framebuffer()
+        pseed = (seed + k * 0x9E3779B9) & 0xFFFFFFFF
+        ref = O.render(s.desc, cam, g.make_params(spp, depth, seed=pseed, buckets=buckets), fp32=True)
+        mse = float(np.mean((acc.astype(np.float64) / spp - ref / spp) ** 2))
+        assert mse < 1e-4, f"pass {k}: mse {mse:.3e}"
+        assert np.array_equal(fb, O.tonemap(acc, spp)), f"pass {k}: framebuffer is not the quantised accumulation"
+        same = float(np.mean(fb == O.tonemap(ref.astype(np.float32), spp)))
+        print(f"{name} pass {k} ({spp} spp, depth {depth}): mse {mse:.2e}, RGBA8 bytes equal to the oracle's {same:.5f}")
+        assert same >= 0.99, f"pass {k}: only {same:.4f} of the RGBA8 bytes match the oracle"
+        assert (fb[..., 3] == 255).all()
     out = tmp_path / "image.png"
     r.save_image(str(out))
-    assert out.stat().st_size > 64 * 64 * 4
+    assert np.array_equal(read_png(str(out)), r.framebuffer())
 
 
 @pytest.mark.parametrize("rings,cols", [(60, 80), (0, 0)])
