@@ -1,24 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s (pixels x spp / s) of the path-tracing hot path.
 
-Workload (N=1 and every N): CornellBoxLucy (scenes.go:714-817) overridden to
-1200x675, 500 spp, depth 5 — the configuration BASELINE.json's roofline
-target is quoted on — with the deterministic synthetic 280K-triangle Lucy
-stand-in (the real mesh is a Git-LFS pointer).  One step =
-one full-quality render of the frame (every pixel x every sample), scene
-already resident in HBM, output a device float3 accumulation buffer.
+Workload (`value`, N=1 and every N): CornellBoxLucy (scenes.go:714-817)
+overridden to 1200x675, 500 spp, depth 5 — BASELINE.json config C4, the one
+its roofline target is quoted on — with the deterministic synthetic
+280K-triangle Lucy stand-in (the real mesh is a Git-LFS pointer, SURVEY.md
+§0.5).  One step = one full-quality render of the frame (every pixel x every
+sample), scene already resident in HBM, output a device float3 accumulation
+buffer.
+
+Also on the same line (`configs`): short timed runs of the other GPU configs
+of BASELINE.json at their stated sizes — C2 RandomScene 1200x675x500 spp
+(depth 50), C3 CornellBoxScene 600x600x1000 spp (depth 5), C5 HDRITestScene
+1920x1080x2000 spp (depth 20) — through the same sharded path.
 
 Multi-GPU (torchrun, one rank per GPU): the 32x32 buckets of the frame are
 dealt round-robin to ranks; each rank renders its buckets into a zeroed
 full-frame buffer, then one RCCL reduce(sum) to rank 0 combines them (each
 pixel has exactly one contributor).  Total work is fixed: strong scaling.
+At N=1, `shard_balance` times the 2/4/8-way round-robin shards of the frame
+one after another on the one GPU and predicts the N-GPU speed-up from the
+slowest shard.
 
-Output: one JSON line on rank 0 (contract in the task statement), with
-`roofline` for the render kernel (algorithmic bytes per launch from the
-instrumented kernel's traversal counts x the per-unit sizes of SURVEY.md
-§8(d) / DESIGN.md, over the render kernel's HIP-event time measured on its
-stream) and `cpu_baseline` (the CPU oracle's fp64 restatement of the Go path,
-multithreaded, on a bounded sample of the same workload; rank 0, N=1 only).
+`roofline`: the dominant kernel's algorithmic bytes per launch (instrumented
+work counts x the per-unit sizes of DESIGN.md §4, stream bytes included) over
+its HIP-event launch time measured on the render stream; `kernels` has the
+same for extend / shade / shadow, plus the HBM traffic of the PMC profile
+(profiles/pmc_<scene>_<W>x<H>.json, tools/profile_round.sh) as `hbm_frac`.
+`cpu_baseline`: the CPU oracle's fp64 restatement of the Go path on every host
+core available to the job, on a bounded sample of the same workload (rank 0,
+N=1 only).
 """
 from __future__ import annotations
 
@@ -31,7 +42,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Algorithmic bytes per unit of work (SURVEY.md §8(d); DESIGN.md §Measurement).
+# Algorithmic bytes per unit of work (SURVEY.md §8(d); DESIGN.md §4).
 BYTES = {
     "node_visits": 128,      # one BVH4 node = four 24-B child boxes + four child items
     "tri_tests": 36,         # v0, e1, e2 fp32
@@ -44,13 +55,22 @@ BYTES = {
     "material_fetches": 32,
     "env_lookups": 48,       # 4 texels x 12 B
 }
-ACCUM_BYTES_PER_SAMPLE = 12
-# Per-ray state each wavefront kernel streams:
-# extend: queue entry 4 + ray o,d 32 + hit record 16 = 52 B per ray;
-# shadow: direction 16 + pending contribution 16 + a share of the per-path
-# origin / throughput / L read-modify-write 16 = 48 B per shadow ray.
-RAY_IO_BYTES = {"extend": 52, "shadow": 48}
+# Path-stream bytes per unit.
+EXTEND_RAY_IO = 48           # ray o, d in (32) + hit record out (16); +16 (throughput word) with volumes
+SHADE_PATH_IN = 80           # hit, o, d, throughput, L of every shaded path
+SHADE_SURVIVOR_OUT = 64      # o, d, throughput, L of the next stream
+SHADE_END_OUT = 16           # Lout of an ended path (once per sample)
+SHADE_JOB_OUT = 68           # NEE job: origin, area dir, info, contribution, throughput (+32 with HDRI IS)
+SHADOW_JOB_IO = 40           # job origin, area dir, info in, visibility out (+16 with HDRI IS)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# BASELINE.json configs run on the GPU (C1 SimpleScene is the CPU plumbing case).
+CONFIGS = {
+    "C2": ("random", dict(width=1200, aspect=16.0 / 9.0, spp=500)),   # depth 50 (scenes.go:72-73)
+    "C3": ("cornell", dict(width=600, aspect=1.0, spp=1000)),         # depth 5
+    "C4": ("cornell-lucy", dict(width=1200, aspect=16.0 / 9.0, spp=500)),
+    "C5": ("hdri-test", dict(width=1920, aspect=16.0 / 9.0, spp=2000)),  # depth 20
+}
 
 
 def parse():
@@ -69,33 +89,202 @@ def parse():
                          "(build.hip); the world BVH is SAH except for 'reference'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented count run")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C2/C3/C5 runs")
+    ap.add_argument("--no-balance", action="store_true", help="skip the shard-balance timing")
+    ap.add_argument("--config-steps", type=int, default=2)
     ap.add_argument("--cpu-spp", type=int, default=48, help="spp of the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every host core available to the job")
     return ap.parse_args()
+
+
+def host_cores():
+    """CPUs this job may use: the affinity mask (what Go's runtime.NumCPU
+    reports, main.go:84), capped by a cgroup CPU quota when one is set."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return cores, aff, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+class Dist:
+    """One process per GPU (RANK/LOCAL_RANK/WORLD_SIZE from torchrun)."""
+
+    def __init__(self):
+        import torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # RTGPU_BENCH_BACKEND=gloo (ranks sharing the visible GPUs) rehearses
+        # the multi-rank path on a one-GPU box
+        self.backend = os.environ.get("RTGPU_BENCH_BACKEND", "nccl")
+        ndev = max(torch.cuda.device_count(), 1)
+        self.dev_index = local % ndev if self.world > 1 else 0
+        torch.cuda.set_device(self.dev_index)
+        self.dev = torch.device("cuda", self.dev_index)
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group(self.backend)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def reduce_frame(self, accum):
+        if self.dist is None:
+            return
+        if self.backend == "nccl":
+            self.dist.reduce(accum, dst=0, op=self.dist.ReduceOp.SUM)   # RCCL over xGMI
+        else:
+            host = accum.cpu()
+            self.dist.reduce(host, dst=0, op=self.dist.ReduceOp.SUM)
+            if self.rank == 0:
+                accum.copy_(host)
+
+
+class Workload:
+    """One scene resident on this rank's GPU, this rank's bucket shard."""
+
+    def __init__(self, g, D: Dist, scene: str, scene_kw: dict, seed: int, blas: str):
+        import torch
+        self.g, self.D = g, D
+        t = time.time()
+        self.scene = g.Scene(scene, **scene_kw)
+        cam = self.cam = self.scene.camera
+        self.W, self.H = cam.image_width, cam.image_height
+        self.spp, self.depth = cam.samples_per_pixel, cam.max_depth
+        self.ctx = g.Context(D.dev_index)
+        self.ctx.set_blas_builder(blas)
+        self.ctx.set_tlas_builder("reference" if blas == "reference" else "sah")
+        self.ctx.upload(self.scene.desc)
+        self.info = self.ctx.info()
+        self.dev_build_ms = self.ctx.last_build_ms()
+        self.build_s = time.time() - t
+        self.seed = seed
+        self.buckets = g.generate_buckets(self.W, self.H, 32)
+        self.params = g.make_params(self.spp, self.depth, seed=seed,
+                                    buckets=g.shard_buckets(self.buckets, D.rank, D.world))
+        self.accum = torch.zeros(self.H * self.W * 3, dtype=torch.float32, device=D.dev)
+        self.stream = torch.cuda.current_stream(D.dev)
+        self.kernel_ms, self.kernel_times = [], []
+
+    def step(self, timed: bool = False, kernel_timing: bool = False):
+        self.accum.zero_()
+        self.ctx.render_device(self.cam, self.params, self.accum.data_ptr(), self.stream.cuda_stream)
+        if timed:
+            # blocks until the render kernel has finished; raises on a device error
+            self.kernel_ms.append(self.ctx.last_render_kernel_ms())
+            if kernel_timing:
+                self.kernel_times.append(self.ctx.last_kernel_times())
+        self.D.reduce_frame(self.accum)
+
+    def run(self, steps: int, warmup: int, kernel_timing: bool = False) -> float:
+        """Barrier + synchronize on both sides of exactly `steps` timed steps;
+        returns the slowest rank's elapsed seconds."""
+        import torch
+        self.ctx.set_kernel_timing(kernel_timing)
+        for _ in range(warmup):
+            self.step()
+        self.ctx.sync()
+        self.D.barrier()
+        torch.cuda.synchronize(self.D.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step(True, kernel_timing)
+        torch.cuda.synchronize(self.D.dev)
+        self.D.barrier()
+        return self.D.max(time.perf_counter() - t0)
+
+    def frame_sum(self):
+        # identical for any rank count: each pixel has one contributor and the
+        # RNG is keyed by global pixel id
+        return float(self.accum.double().sum().item()) if self.D.rank == 0 else None
+
+    def samples(self) -> int:
+        return self.W * self.H * self.spp
+
+    def close(self):
+        self.ctx.close()
+
+
+def kernel_report(w: Workload, work_k: dict, pmc: dict | None):
+    """Per-kernel algorithmic bytes (work counts x per-unit bytes, stream bytes
+    included) and achieved GB/s over the HIP-event launch times; HBM traffic
+    and its fraction of peak from the PMC profile when it is for this code."""
+    import numpy as np
+    ext, sha, shd = work_k["extend"], work_k["shade"], work_k["shadow"]
+    info = w.info
+    envis = False
+    try:
+        d = w.scene.desc.contents
+        envis = bool(d.environment) and bool(d.environment.contents.use_importance_sampling) and d.num_lights > 0
+    except (ValueError, AttributeError):
+        pass
+    vol = info.volumes > 0
+    samples = ext["samples"]
+    trav = {k: sum(BYTES[u] * wk[u] for u in BYTES) for k, wk in (("extend", ext), ("shade", sha), ("shadow", shd))}
+    alg = {
+        "extend": trav["extend"] + (EXTEND_RAY_IO + (16 if vol else 0)) * ext["rays"],
+        "shade": trav["shade"] + SHADE_PATH_IN * sha["rays"] + SHADE_SURVIVOR_OUT * (ext["rays"] - samples)
+                 + SHADE_END_OUT * samples + (SHADE_JOB_OUT + (32 if envis else 0)) * sha["shadow_rays"],
+        "shadow": trav["shadow"] + (SHADOW_JOB_IO + (16 if envis else 0)) * sha["shadow_rays"],
+    }
+    out = {}
+    for k in ("extend", "shade", "shadow"):
+        launches = int(np.mean([t[f"{k}_launches"] for t in w.kernel_times]))
+        ms_tot = float(np.mean([t[f"{k}_ms"] for t in w.kernel_times]))
+        ms_avg = ms_tot / max(launches, 1)
+        per_launch = alg[k] / max(launches, 1)
+        e = {"launches": launches, "ms_total": round(ms_tot, 3), "ms_avg": round(ms_avg, 4),
+             "alg_bytes_per_launch": int(per_launch),
+             "achieved_GBs": round(per_launch / (ms_avg / 1e3) / 1e9, 2) if ms_avg > 0 else None}
+        e["frac"] = round(e["achieved_GBs"] / HBM_PEAK_GBS, 4) if e["achieved_GBs"] else None
+        kp = (pmc or {}).get("kernels", {}).get(k)
+        if kp and ms_avg > 0:
+            tb = kp["hbm_bytes_per_launch"]
+            e["traffic_bytes_per_launch"] = int(tb)
+            e["hbm_GBs"] = round(tb / (ms_avg / 1e3) / 1e9, 2)
+            e["hbm_frac"] = round(e["hbm_GBs"] / HBM_PEAK_GBS, 4)
+            # share of the algorithmic bytes served without an HBM transfer
+            # (negative: more HBM traffic than the algorithm's bytes)
+            e["l2_served"] = round(1.0 - tb / per_launch, 4) if per_launch > 0 else None
+        out[k] = e
+    return out
 
 
 def main():
     args = parse()
     import numpy as np
-    import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # one rank per GPU; RTGPU_BENCH_BACKEND=gloo (with ranks sharing the
-    # visible GPUs) rehearses the multi-rank path on a one-GPU box
-    backend = os.environ.get("RTGPU_BENCH_BACKEND", "nccl")
-    ndev = max(torch.cuda.device_count(), 1)
-    dev_index = local % ndev if world > 1 else 0
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(dev_index)
-        dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", dev_index)
-
+    D = Dist()
     import __graft_entry__ as ge
     g = ge.load_package()
 
@@ -108,126 +297,116 @@ def main():
         scene_kw["spp"] = args.spp
     if args.depth:
         scene_kw["max_depth"] = args.depth
-    t_build = time.time()
-    scene = g.Scene(args.scene, **scene_kw)
-    cam = scene.camera
-    W, H, spp, depth = cam.image_width, cam.image_height, cam.samples_per_pixel, cam.max_depth
-    ctx = g.Context(dev_index)
-    ctx.set_blas_builder(args.blas)
-    ctx.set_tlas_builder("reference" if args.blas == "reference" else "sah")
-    ctx.upload(scene.desc)
-    info = ctx.info()
-    t_build = time.time() - t_build
-
-    buckets = g.generate_buckets(W, H, 32)
-    mine = g.shard_buckets(buckets, rank, world)
-    params = g.make_params(spp, depth, seed=args.seed, buckets=mine)
-    accum = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    kernel_ms = []
-    kernel_times = []
-
-    def step(timed: bool):
-        accum.zero_()
-        ctx.render_device(cam, params, accum.data_ptr(), stream.cuda_stream)
-        if timed:
-            kernel_ms.append(ctx.last_render_kernel_ms())
-            kernel_times.append(ctx.last_kernel_times())
-        if dist is not None:
-            if backend == "nccl":
-                dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)   # RCCL over xGMI
-            else:
-                host = accum.cpu()
-                dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
-                if rank == 0:
-                    accum.copy_(host)
+    w = Workload(g, D, args.scene, scene_kw, args.seed, args.blas)
+    W, H, spp, depth = w.W, w.H, w.spp, w.depth
 
     # one HIP event before each extend/shade/shadow launch (and after each
     # shadow launch) on the render stream: per-kernel launch durations
-    ctx.set_kernel_timing(True)
-    for _ in range(args.warmup):
-        step(False)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    samples_per_step = W * H * spp
-    value = samples_per_step * args.steps / elapsed / 1e6
+    elapsed = w.run(args.steps, args.warmup, kernel_timing=True)
+    value = w.samples() * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
-    img_ok = bool(torch.isfinite(accum).all().item()) if rank == 0 else True
-    # checksum of the combined frame: identical for any rank count (each pixel
-    # has one contributor and the RNG is keyed by global pixel id)
-    frame_sum = float(accum.double().sum().item()) if rank == 0 else None
+    img_ok = bool(__import__("torch").isfinite(w.accum).all().item()) if D.rank == 0 else True
+    frame_sum = w.frame_sum()
 
     roofline = None
-    work = None
     kernels = None
-    if rank == 0 and not args.no_count:
-        work_k = ctx.count_work_by_kernel(cam, params)
-        work = {k: sum(w[k] for w in work_k.values()) for k in work_k["extend"]}
-        kernels = {}
-        for kname in ("extend", "shade", "shadow"):
-            wk = work_k[kname]
-            alg = sum(BYTES[k] * wk[k] for k in BYTES)
-            if kname == "extend":
-                alg += RAY_IO_BYTES["extend"] * wk["rays"]
-            elif kname == "shadow":
-                alg += RAY_IO_BYTES["shadow"] * wk["shadow_rays"]
-            launches = int(np.mean([t[f"{kname}_launches"] for t in kernel_times]))
-            ms_tot = float(np.mean([t[f"{kname}_ms"] for t in kernel_times]))
-            kernels[kname] = {"launches": launches, "ms_total": round(ms_tot, 3),
-                              "ms_avg": round(ms_tot / max(launches, 1), 4),
-                              "alg_bytes_per_launch": int(alg / max(launches, 1)),
-                              "achieved_GBs": round(alg / (ms_tot / 1e3) / 1e9, 2) if ms_tot > 0 else None}
+    work = None
+    if D.rank == 0 and not args.no_count:
+        work_k = w.ctx.count_work_by_kernel(w.cam, w.params)
+        work = {k: work_k["extend"][k] + work_k["shadow"][k] + (0 if k in ("rays", "shadow_rays") else
+                                                                work_k["shade"][k]) for k in work_k["extend"]}
+        pmc, pmc_name = None, f"pmc_{args.scene}_{W}x{H}.json"
+        pmc_path = os.path.join(ROOT, "profiles", pmc_name)
+        pmc_stale = None
+        if os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))
+                ref_sum = pmc.get("frame_sum")
+                pmc_stale = ref_sum is None or frame_sum is None or abs(ref_sum - frame_sum) > 1e-9 * abs(frame_sum)
+            except (OSError, ValueError):
+                pmc = None
+        kernels = kernel_report(w, work_k, pmc)
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
         kd = kernels[dom]
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}.json")
-        if os.path.exists(pmc):
-            try:
-                traffic = json.load(open(pmc))["kernels"][dom]["hbm_bytes_per_launch"]
-            except Exception:
-                traffic = None
         roofline = {"bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "frac": kd["frac"], "traffic": kd.get("traffic_bytes_per_launch"),
+                    "hbm_frac": kd.get("hbm_frac"), "l2_served": kd.get("l2_served"),
                     "kernel": f"k_{dom}", "kernel_ms_avg": kd["ms_avg"], "launches_per_step": kd["launches"],
                     "alg_bytes_per_launch": kd["alg_bytes_per_launch"],
-                    "pipeline_ms_avg": round(float(np.mean(kernel_ms)), 3)}
+                    "traffic_source": pmc_name if pmc else None, "traffic_stale": pmc_stale,
+                    "pipeline_ms_avg": round(float(np.mean(w.kernel_ms)), 3)}
+
+    balance = None
+    if D.world == 1 and not args.no_balance:
+        import torch
+
+        def timed_render(params) -> float:
+            w.accum.zero_()
+            torch.cuda.synchronize(D.dev)
+            t0 = time.perf_counter()
+            w.ctx.render_device(w.cam, params, w.accum.data_ptr(), w.stream.cuda_stream)
+            w.ctx.sync()
+            return (time.perf_counter() - t0) * 1e3
+
+        full = min(timed_render(w.params) for _ in range(2))
+        balance = {"full_frame_ms": round(full, 2)}
+        for n in (2, 4, 8):
+            shard_ms = []
+            for r in range(n):
+                p = g.make_params(spp, depth, seed=args.seed, buckets=g.shard_buckets(w.buckets, r, n))
+                shard_ms.append(min(timed_render(p) for _ in range(2)))
+            mx, mean = max(shard_ms), float(np.mean(shard_ms))
+            balance[f"n{n}"] = {"shard_ms": [round(x, 2) for x in shard_ms], "max_over_mean": round(mx / mean, 4),
+                                "predicted_speedup": round(full / mx, 3)}
+        balance["note"] = ("round-robin 32x32 bucket shards (shard_buckets) timed one after another on this GPU, "
+                           "host clock around render + sync; predicted speed-up = full frame / slowest shard, "
+                           "excluding the RCCL reduce of the frame")
+
+    configs = None
+    if not args.no_configs:
+        # the main workload's buffers are released first (path slots are sized
+        # from the free HBM)
+        main_ctx_closed = True
+        w.close()
+        configs = {}
+        for cid, (scene, kw) in CONFIGS.items():
+            if scene == args.scene and kw["width"] == W and kw["spp"] == spp:
+                configs[cid] = {"workload": f"{scene} {W}x{H} {spp}spp depth {depth}", "value": round(value, 3),
+                                "ms_per_step": round(ms_per_step, 3), "steps": args.steps, "frame_sum": frame_sum}
+                continue
+            cw = Workload(g, D, scene, kw, args.seed, args.blas)
+            el = cw.run(args.config_steps, 1)
+            configs[cid] = {"workload": f"{scene} {cw.W}x{cw.H} {cw.spp}spp depth {cw.depth}",
+                            "value": round(cw.samples() * args.config_steps / el / 1e6, 3),
+                            "ms_per_step": round(el / args.config_steps * 1e3, 3), "steps": args.config_steps,
+                            "frame_sum": cw.frame_sum()}
+            cw.close()
+    else:
+        main_ctx_closed = False
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         from oracle import oracle_py as O
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cores, aff, quota = host_cores()
+        threads = args.cpu_threads or cores
         cpu_spp = args.cpu_spp
         # bounded sample: every pixel of the same frame at cpu_spp samples,
         # same scene/BVH/depth, fp64 (the reference's arithmetic)
         cp = g.make_params(cpu_spp, depth, seed=args.seed)
         tc = time.perf_counter()
-        O.render(scene.desc, cam, cp, fp32=False, threads=threads)
+        O.render(w.scene.desc, w.cam, cp, fp32=False, threads=threads)
         tcpu = time.perf_counter() - tc
         cpu = {"value": round(W * H * cpu_spp / tcpu / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-               "kind": "port",
+               "kind": "port", "cpu_model": cpu_model(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
                "sample": f"{args.scene} {W}x{H} x {cpu_spp} spp depth {depth} (fp64 C restatement of the Go path, "
-                         f"{threads} threads), {tcpu:.1f} s"}
+                         f"{threads} threads = every CPU available to the job), {tcpu:.1f} s"}
 
-    if rank == 0:
+    if D.rank == 0:
         line = {
             "metric": "Msamples/sec (pixels x SPP / s)",
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": D.world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -238,9 +417,9 @@ def main():
             "data": "synthetic (deterministic 280K-tri Lucy stand-in; scene geometry per scenes.go)",
             "config": {"workload": f"{args.scene} {W}x{H} {spp}spp depth {depth}", "scene": args.scene,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "parallelism": f"tiles-rr{world}", "buckets": len(buckets), "blas": args.blas,
-                       "triangles": info.triangles, "bvh_nodes": info.nodes,
-                       "scene_build_s": round(t_build, 2), "device_bvh_build_ms": round(ctx.last_build_ms(), 2),
+                       "parallelism": f"tiles-rr{D.world}", "buckets": len(w.buckets), "blas": args.blas,
+                       "triangles": w.info.triangles, "bvh_nodes": w.info.nodes,
+                       "scene_build_s": round(w.build_s, 2), "device_bvh_build_ms": round(w.dev_build_ms, 2),
                        "image_finite": img_ok, "frame_sum": frame_sum},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -250,11 +429,16 @@ def main():
         if work is not None:
             line["work_per_sample"] = {k: round(v / max(work["samples"], 1), 3) for k, v in work.items()
                                        if k != "samples"}
+        if configs is not None:
+            line["configs"] = configs
+        if balance is not None:
+            line["shard_balance"] = balance
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    ctx.close()
+    D.barrier()
+    if D.dist is not None:
+        D.dist.destroy_process_group()
+    if not main_ctx_closed:
+        w.close()
 
 
 if __name__ == "__main__":

@@ -706,6 +706,8 @@ int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params
   rt_work_counts k[3];
   int rc = rt_count_work_by_kernel(ctx, cam, params, k);
   if (rc) return rc;
+  k[1].rays = 0;          // shade's: paths shaded (the extend rays again)
+  k[1].shadow_rays = 0;   // shade's: NEE jobs (the shadow kernel counts the rays)
   const uint64_t* a = reinterpret_cast<const uint64_t*>(&k[0]);
   const uint64_t* b = reinterpret_cast<const uint64_t*>(&k[1]);
   const uint64_t* d = reinterpret_cast<const uint64_t*>(&k[2]);

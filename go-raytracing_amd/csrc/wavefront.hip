@@ -278,6 +278,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
     float time = 0.0f, tmax_a = 0.0f;
     V3 L = mk(0.0f, 0.0f, 0.0f), P = L, sd = L, beta = L, nbeta = L, ca = L, ch = L, da = L, dh = L;
     if (live) {
+      if (kCount) cnt.rays++;                                    // paths shaded
       const uint32_t ii = GIX(i, a.slots, 41);
       const float4 h = ldnt(&a.hit[ii]), o4 = ldnt(&cs.o[ii]), d4 = ldnt(&cs.d[ii]), b4 = ldnt(&cs.beta[ii]),
                    L4 = ldnt(&cs.L[ii]);
@@ -445,6 +446,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
       stnt(&a.Lout[slot], make_float4(L.x, L.y, L.z, 0.0f));
     }
     if (want_shadow) {
+      if (kCount) cnt.shadow++;                                  // NEE jobs written
       js = GIX(js, a.slots, 45);
       stnt(&a.sj_p[js], make_float4(P.x, P.y, P.z, asf(key)));
       stnt(&a.sj_a[js], make_float4(da.x, da.y, da.z, tmax_a));

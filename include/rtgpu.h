@@ -301,7 +301,9 @@ int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params
 
 /* Same instrumented run, counters split by kernel: out[0] = extend
  * (closest-hit traversal, camera rays), out[1] = shade (materials, NEE
- * set-up, HDRI lookups), out[2] = shadow (any-hit traversal).             */
+ * set-up, HDRI lookups; there `rays` counts the paths shaded and
+ * `shadow_rays` the NEE jobs written), out[2] = shadow (any-hit traversal).
+ * rt_count_work's `rays` / `shadow_rays` are the extend and shadow ones.   */
 int rt_count_work_by_kernel(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                             rt_work_counts out[3]);
 

@@ -17,7 +17,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGS = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-count", "--width", "320", "--spp", "8"]
+ARGS = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-count", "--no-configs", "--no-balance",
+        "--width", "320", "--spp", "8"]
 
 
 def _port():

@@ -3,7 +3,7 @@
 # GPU, gloo carries the reduce; the frame checksum must equal the N=1 run.
 set -o pipefail
 mkdir -p gpurun_out
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-count --spp ${SPP:-64}"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-count --no-configs --no-balance --spp ${SPP:-64}"
 timeout -k 10 300 python3 bench.py $ARGS > gpurun_out/mr_1.json 2> gpurun_out/mr_1.err || { tail -20 gpurun_out/mr_1.err; exit 1; }
 for n in 2 4; do
   RTGPU_BENCH_BACKEND=gloo timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n \

@@ -48,6 +48,8 @@ except Exception:
 cfg = bench.get("config", {})
 out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --steps 1 --warmup 0 (default workload: the timed steps' per-launch batches)",
        "scene": cfg.get("scene", "cornell-lucy"), "width": cfg.get("width"), "height": cfg.get("height"),
+       # the frame this code renders: bench.py marks the traffic stale when it changes
+       "frame_sum": cfg.get("frame_sum"),
        "kernels": {}}
 for fam, v in vals.items():
     n = max(len(disp[fam]["FETCH_SIZE"]), 1)

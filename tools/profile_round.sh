@@ -11,9 +11,9 @@ export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
-  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
+  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs --no-balance > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o p -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count > $OUT/$c.json 2> $OUT/$c.err || exit 1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-configs --no-balance > $OUT/$c.json 2> $OUT/$c.err || exit 1
 done
 echo done
