@@ -112,7 +112,7 @@ class RtWorkCounts(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "rays", "shadow_rays", "node_visits", "sphere_tests",
                                           "quad_tests", "tri_tests", "plane_tests", "instance_visits",
                                           "volume_tests", "material_fetches", "env_lookups",
-                                          "instance_box_tests")]
+                                          "instance_box_tests", "stack_spills")]
 
 
 class RtKernelTimes(C.Structure):

@@ -236,10 +236,8 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // 32M 686, 128M 759, 210M 799, the whole 405M-sample frame in one batch
   // 833.  Samples are split evenly over the batches.  RTGPU_SLOTS overrides
   // (tuning knob).
-  // Per slot: two path streams (4 x 16 B each), hit, Lout, six NEE job
-  // fields (16 B each), job info + visibility words.
-  constexpr size_t kSlotF4 = 16;
-  constexpr size_t kSlotBytes = kSlotF4 * sizeof(float4) + 2 * sizeof(uint32_t);
+  // Per slot: kSlotF4 float4 arrays (wavefront.h) + job info + visibility words.
+  constexpr size_t kSlotBytes = size_t(kSlotF4) * sizeof(float4) + 2 * sizeof(uint32_t);
   static const size_t env_slots = [] {
     const char* e = getenv("RTGPU_SLOTS");
     return e && atol(e) > 0 ? size_t(atol(e)) : size_t(0);
@@ -260,7 +258,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
     ctx->wslots = 0;
-    if ((rc = ensure(ctx, ctx->wstate, nslots * kSlotF4 * sizeof(float4)))) return rc;
+    if ((rc = ensure(ctx, ctx->wstate, nslots * size_t(kSlotF4) * sizeof(float4)))) return rc;
     if ((rc = ensure(ctx, ctx->wq, nslots * 2 * sizeof(uint32_t) + CNT_WORDS_Q * sizeof(uint32_t)))) return rc;
     ctx->wslots = nslots;
   }
@@ -284,12 +282,12 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   float4* base = static_cast<float4*>(ctx->wstate.p);
   const size_t S = ctx->wslots;
   for (int k = 0; k < 2; ++k) {
-    float4* sb = base + size_t(4 * k) * S;
-    a.s[k] = PathStream{sb, sb + S, sb + 2 * S, sb + 3 * S};
+    float4* sb = base + size_t(3 * k) * S;
+    a.s[k] = PathStream{sb, sb + S, sb + 2 * S};
   }
-  a.hit = base + 8 * S; a.Lout = base + 9 * S;
-  a.sj_p = base + 10 * S; a.sj_a = base + 11 * S; a.sj_h = base + 12 * S;
-  a.ne_a = base + 13 * S; a.ne_h = base + 14 * S; a.ne_beta = base + 15 * S;
+  a.hit = base + 6 * S; a.Lout = base + 7 * S;
+  a.sj_p = base + 8 * S; a.sj_a = base + 9 * S; a.sj_h = base + 10 * S;
+  a.ne_a = base + 11 * S; a.ne_h = base + 12 * S; a.ne_beta = base + 13 * S;
   uint32_t* qb = static_cast<uint32_t*>(ctx->wq.p);
   a.counts = qb;
   a.sj_info = qb + CNT_WORDS_Q;
@@ -582,6 +580,8 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;
   if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }
+  build_inst_entries(h);   // BLAS roots are final now
+  if ((rc = upload_vec(ctx, h.inst_entries, &d.inst_entry))) { free_scene(ctx); return rc; }
   ctx->has_scene = true;
   return RT_OK;
 }
@@ -686,6 +686,7 @@ void fill_counts(const unsigned long long* c, rt_work_counts* out) {
   out->material_fetches = c[10];
   out->env_lookups = c[11];
   out->instance_box_tests = c[12];
+  out->stack_spills = c[13];
 }
 }  // namespace
 

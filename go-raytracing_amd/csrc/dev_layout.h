@@ -87,6 +87,8 @@ struct alignas(16) DNode4 {
 // The traversal addresses nodes by 32-bit byte offset (index << 7): at most
 // 2^25 BVH4 nodes per scene (flatten / device_builds refuse more).
 constexpr uint32_t kMaxNodes4 = 1u << 25;
+static_assert(sizeof(DNode4) == 128 && uint64_t(kMaxNodes4) * sizeof(DNode4) == (uint64_t(1) << 32),
+              "32-bit node byte offsets");
 
 struct alignas(8) DLeaf {
   uint32_t first;  // index into refs (PK_MIXED) or into the kind's prim array
@@ -145,6 +147,24 @@ struct alignas(16) DInstance {
   int32_t pad2, pad3;
   float prm[MAX_WRAP][6];    // translate: off xyz; rot: sin, cos; scale: f xyz, invf xyz
 };
+
+// Instance entry record, one per TLAS ref position (ITEM_INSTANCE items
+// carry the ref position): everything the traversal needs to enter the
+// instance in ONE 128-B line — the wrapper chain's ray-side parameters (the
+// same floats DInstance holds, in the same wrapper order) and the BLAS root
+// item and box — instead of the dependent refs -> DInstance -> DBvh loads.
+// Built from DInstance / DBvh by build_inst_entries (flatten.cpp) after any
+// device BLAS build.  Non-instance refs have nwrap 0 and are never read.
+struct alignas(128) DInstEntry {
+  float box[6];              // BLAS root box (object space)
+  uint32_t root_item;
+  int32_t check_box;
+  uint32_t kinds;            // wrapper kind i in bits 4i..4i+3 (outermost first)
+  int32_t nwrap;
+  float prm[MAX_WRAP][3];    // translate: offset; rotate: sin, cos, -; scale: 1/factor
+  float pad[4];
+};
+static_assert(sizeof(DInstEntry) == 128, "DInstEntry is one 128-B line");
 
 struct alignas(16) DVolume {   // volume.go:9-13
   int32_t boundary;          // instance index describing the boundary (chain + list)
@@ -227,6 +247,7 @@ struct DScene {
   const float* image_texels;   // 4 floats per texel: rgb (w unused), all images back to back
   const DPlane* planes;
   const DInstance* instances;
+  const DInstEntry* inst_entry;  // per TLAS ref position (instance refs)
   const DBvh* blas;
   const DVolume* volumes;
   const DMaterial* materials;

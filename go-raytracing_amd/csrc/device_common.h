@@ -258,36 +258,42 @@ __device__ __forceinline__ bool plane_t(const DPlane& p, V3 o, V3 d, float tmin,
 // ----------------------------------------------------------------------------
 // Transform wrapper chain (transform.go), outermost wrapper first.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ void wrap_ray(int kind, const float* p, V3& o, V3& d) {
+// Ray into the wrapper's space; (a, b, c) = the wrapper's ray-side floats:
+// translate offset, rotation (sin, cos, -), scale 1/factor.
+__device__ __forceinline__ void wrap_ray3(int kind, float a, float b, float c, V3& o, V3& d) {
   switch (kind) {
-    case W_TRANSLATE: o = sub(o, mk(p[0], p[1], p[2])); break;                    // :94
+    case W_TRANSLATE: o = sub(o, mk(a, b, c)); break;                              // :94
     case W_ROT_Y: {                                                                  // :163-167
-      float s = p[0], c = p[1];
+      const float s = a, cs = b;
       V3 no = o, nd = d;
-      no.x = c * o.x - s * o.z; no.z = s * o.x + c * o.z;
-      nd.x = c * d.x - s * d.z; nd.z = s * d.x + c * d.z;
+      no.x = cs * o.x - s * o.z; no.z = s * o.x + cs * o.z;
+      nd.x = cs * d.x - s * d.z; nd.z = s * d.x + cs * d.z;
       o = no; d = nd; break;
     }
     case W_ROT_X: {                                                                  // :233-237
-      float s = p[0], c = p[1];
+      const float s = a, cs = b;
       V3 no = o, nd = d;
-      no.y = c * o.y - s * o.z; no.z = s * o.y + c * o.z;
-      nd.y = c * d.y - s * d.z; nd.z = s * d.y + c * d.z;
+      no.y = cs * o.y - s * o.z; no.z = s * o.y + cs * o.z;
+      nd.y = cs * d.y - s * d.z; nd.z = s * d.y + cs * d.z;
       o = no; d = nd; break;
     }
     case W_ROT_Z: {                                                                  // :314-318
-      float s = p[0], c = p[1];
+      const float s = a, cs = b;
       V3 no = o, nd = d;
-      no.x = c * o.x - s * o.y; no.y = s * o.x + c * o.y;
-      nd.x = c * d.x - s * d.y; nd.y = s * d.x + c * d.y;
+      no.x = cs * o.x - s * o.y; no.y = s * o.x + cs * o.y;
+      nd.x = cs * d.x - s * d.y; nd.y = s * d.x + cs * d.y;
       o = no; d = nd; break;
     }
     case W_SCALE:                                                                    // :409-418
-      o = mk(o.x * p[3], o.y * p[4], o.z * p[5]);
-      d = mk(d.x * p[3], d.y * p[4], d.z * p[5]);
+      o = mk(o.x * a, o.y * b, o.z * c);
+      d = mk(d.x * a, d.y * b, d.z * c);
       break;
     default: break;
   }
+}
+__device__ __forceinline__ void wrap_ray(int kind, const float* p, V3& o, V3& d) {
+  if (kind == W_SCALE) wrap_ray3(kind, p[3], p[4], p[5], o, d);
+  else wrap_ray3(kind, p[0], p[1], p[2], o, d);
 }
 // Back-map of the hit point and normal (inner wrapper first).
 __device__ __forceinline__ void unwrap_hit(int kind, const float* p, V3& P, V3& N) {
@@ -379,7 +385,7 @@ __device__ __forceinline__ bool accept(const DScene& sc, float t, int kind, int 
 
 // Work counters for the instrumented variant (rt_count_work).
 struct Cnt {
-  uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env, ibox;
+  uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env, ibox, spill;
 };
 
 // Volume.Hit (volume.go:34-79) against a boundary given as an instance chain
@@ -574,6 +580,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   // overflow is an internal error: flagged for the host, the entry dropped,
   // and no early exit in the push sequence.
   auto push = [&](uint32_t v) {
+    if (kCount && T.sp >= S.cap) cnt.spill++;
     if (T.sp < S.cap + S.spill_cap) { S.push(T.sp, v); ++T.sp; }
     else *err = 1;
   };
@@ -595,6 +602,12 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const float4 nx = ldn(nb + sxo), fx = ldn(nb + (16u - sxo)), ny = ldn(nb + (32u + syo)), fy = ldn(nb + (48u - syo));
     const float4 nz = ldn(nb + (64u + szo)), fz = ldn(nb + (80u - szo));
     const uint4 it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
+#if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
+    // issue the child-item load with the plane loads (same 128-B line): the
+    // compiler otherwise sinks it into the "a child was hit" branch, which
+    // costs a second dependent round trip per node
+    asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));
+#endif
     if (kCount) cnt.nodes++;
     const float hi = kAny ? T.tmax : best.t;
     const float inf = __builtin_inff();
@@ -689,24 +702,60 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         }
       }
     } else if (tag == ITEM_INSTANCE) {
-      const uint32_t r = sc.refs[GIX(idx, sc.n_refs, 17)];
-      const int ii = int(r & REF_MASK);
-      const DInstance& in = sc.instances[GIX(ii, sc.n_instances, 18)];
-      if (kCount) cnt.inst++;
-      V3 o = S.wo(), d = S.wd();
-      to_object(in, o, d);
-      const TRay orr = make_tray(o, d);
-      const DBvh& bb = sc.blas[GIX(in.blas, sc.n_blas, 19)];
-      bool enter = true;
-      float tn = 0.0f;
-      if (bb.check_box)
-        enter = box_hit(bb.box[0], bb.box[1], bb.box[2], bb.box[3], bb.box[4], bb.box[5], orr, T.tmin,
-                        kAny ? T.tmax : best.t, tn);
-      if (enter) {
-        if (T.item < ITEM_POP) push(T.item);
-        push(ITEM_INST_END << ITEM_SHIFT);
-        T.cr = orr; T.cur_ref = int(idx);
-        T.item = bb.root_item;
+      // one 128-B entry record per instance ref (DInstEntry): the wrapper
+      // chain's ray-side floats and the BLAS root in one line, instead of the
+      // dependent refs -> DInstance -> DBvh loads.  The any-hit kernel loads
+      // it as five float4s issued together; the closest-hit kernel, whose
+      // registers are tighter (the hit record), field by field (measured:
+      // each form is the faster one in its kernel).
+      if constexpr (!kAny) {
+        const DInstEntry& E = sc.inst_entry[GIX(idx, sc.n_refs, 17)];
+        if (kCount) cnt.inst++;
+        V3 o = S.wo(), d = S.wd();
+        const uint32_t kinds = E.kinds;
+        const int nwrap = E.nwrap;
+        for (int i = 0; i < nwrap; ++i) wrap_ray3(int((kinds >> (4 * i)) & 15u), E.prm[i][0], E.prm[i][1], E.prm[i][2], o, d);
+        const TRay orr = make_tray(o, d);
+        bool enter = true;
+        float tn = 0.0f;
+        if (E.check_box)   // BVHNode.Hit tests its own bbox first
+          enter = box_hit(E.box[0], E.box[1], E.box[2], E.box[3], E.box[4], E.box[5], orr, T.tmin, best.t, tn);
+        if (enter) {
+          if (T.item < ITEM_POP) push(T.item);
+          push(ITEM_INST_END << ITEM_SHIFT);
+          T.cr = orr; T.cur_ref = int(idx);
+          T.item = E.root_item;
+        }
+      } else {
+        const float4* e4 = reinterpret_cast<const float4*>(sc.inst_entry + GIX(idx, sc.n_refs, 17));
+        const float4 h0 = e4[0], h1 = e4[1], h2 = e4[2], q3 = e4[3], q4 = e4[4];
+        if (kCount) cnt.inst++;
+        const uint32_t kinds = __float_as_uint(h2.x);
+        const int nwrap = int(__float_as_uint(h2.y));
+        V3 o = S.wo(), d = S.wd();
+        auto wr = [&](int i, float a, float b, float c) {
+          if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), a, b, c, o, d);
+        };
+        wr(0, h2.z, h2.w, q3.x);
+        wr(1, q3.y, q3.z, q3.w);
+        wr(2, q4.x, q4.y, q4.z);
+        if (nwrap > 3) {
+          const float4 q5 = e4[5], q6 = e4[6];
+          wr(3, q4.w, q5.x, q5.y);
+          wr(4, q5.z, q5.w, q6.x);
+          wr(5, q6.y, q6.z, q6.w);
+        }
+        const TRay orr = make_tray(o, d);
+        bool enter = true;
+        float tn = 0.0f;
+        if (__float_as_uint(h1.w) != 0u)   // check_box: BVHNode.Hit tests its own bbox first
+          enter = box_hit(h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, orr, T.tmin, T.tmax, tn);
+        if (enter) {
+          if (T.item < ITEM_POP) push(T.item);
+          push(ITEM_INST_END << ITEM_SHIFT);
+          T.cr = orr; T.cur_ref = int(idx);
+          T.item = __float_as_uint(h1.z);   // BLAS root item
+        }
       }
     } else {  // ITEM_INST_END: back to the world-space ray
       T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
@@ -997,11 +1046,15 @@ __device__ __noinline__ void get_ray_slow(const DCamera& cam, int px, int py, ui
   rd = sub(ps, ro);
 }
 
+// rayTime (camera.go:370): the path key's camera draw 2; the wavefront
+// kernels recompute it from the key instead of carrying it in the streams.
+__device__ __forceinline__ float ray_time(uint32_t key) { return rnd(key, ctr(0, DOM_CAMERA, 2)); }
+
 __device__ __forceinline__ void get_ray(const DCamera& cam, int px, int py, uint32_t key, V3& ro, V3& rd,
                                         float& time) {
   float offx = rnd(key, ctr(0, DOM_CAMERA, 0)) - 0.5f;
   float offy = rnd(key, ctr(0, DOM_CAMERA, 1)) - 0.5f;
-  time = rnd(key, ctr(0, DOM_CAMERA, 2));
+  time = ray_time(key);
   if (cam.slow) { get_ray_slow(cam, px, py, key, offx, offy, time, ro, rd); return; }
   V3 ps = add(add(ld3(cam.pixel00), scale(ld3(cam.du), float(px) + offx)), scale(ld3(cam.dv), float(py) + offy));
   ro = ld3(cam.center);

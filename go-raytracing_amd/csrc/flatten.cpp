@@ -1122,11 +1122,34 @@ struct Flattener {
     size_t dev_room = 0;
     for (const auto& j : S.device_builds) dev_room += j.n;
     if (S.nodes4.size() + dev_room >= kMaxNodes4) fail(RT_ERR_UNSUPPORTED, "scene too large for 32-bit BVH4 node offsets");
+    if (!status) build_inst_entries(S);
     return status;
   }
 };
 
 }  // namespace
+
+void build_inst_entries(HostScene& S) {
+  S.inst_entries.assign(S.refs.size(), DInstEntry{});
+  for (size_t r = 0; r < S.refs.size(); ++r) {
+    if (int(S.refs[r] >> REF_SHIFT) != PK_INSTANCE) continue;
+    const DInstance& in = S.instances[S.refs[r] & REF_MASK];
+    const DBvh& bb = S.blas[size_t(in.blas)];
+    DInstEntry& e = S.inst_entries[r];
+    for (int k = 0; k < 6; ++k) e.box[k] = bb.box[k];
+    e.root_item = bb.root_item;
+    e.check_box = bb.check_box;
+    e.nwrap = in.nwrap;
+    e.kinds = 0;
+    for (int i = 0; i < in.nwrap; ++i) {
+      e.kinds |= uint32_t(in.kind[i]) << (4 * i);
+      // the floats wrap_ray reads (device_common.h): translate p[0..2],
+      // rotations p[0] (sin), p[1] (cos), scale p[3..5] (1/factor)
+      const int o = in.kind[i] == W_SCALE ? 3 : 0;
+      for (int j = 0; j < 3; ++j) e.prm[i][j] = in.prm[i][o + j];
+    }
+  }
+}
 
 int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err, const FlattenOptions& opt) {
   out = HostScene{};

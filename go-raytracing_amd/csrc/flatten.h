@@ -34,6 +34,7 @@ struct HostScene {
   std::vector<DPlane> planes;
   std::vector<int32_t> plane_hidx;
   std::vector<DInstance> instances;
+  std::vector<DInstEntry> inst_entries;   // per ref (build_inst_entries)
   std::vector<DBvh> blas;
   std::vector<DVolume> volumes;
   std::vector<int32_t> volume_hidx;
@@ -72,6 +73,11 @@ struct FlattenOptions {
   int tlas_builder = BLAS_SAH;   // world BVH: SAH over the top-level objects, one per leaf
   int sah_min_prims = 16;   // smaller all-triangle BLASes keep the reference topology
 };
+
+// (Re)builds S.inst_entries from refs / instances / blas headers: call after
+// the BLAS roots are final (flatten_scene does; rt_scene_upload again after
+// the device BLAS builds).
+void build_inst_entries(HostScene& S);
 
 // Returns RT_OK or an rt_status; `err` receives a message.
 int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err,

@@ -9,26 +9,34 @@ namespace rtg {
 // Per-bounce path stream: one dense record per live path, indexed by its
 // position in this bounce's stream (SoA of 16-B fields, one dwordx4 per lane
 // per array, so every kernel reads and writes it coalesced).
+// The ray time (camera.go:370) is not carried: it is the path key's camera
+// draw, recomputed where needed (ray_time).  The radiance is not carried
+// either: it accumulates in place in Lout[slot].
 struct PathStream {
-  float4* o;        // ray origin.xyz, time
+  float4* o;        // ray origin.xyz, path slot (sample_in_batch * npix + pixel_in_list)
   float4* d;        // ray direction.xyz, RNG path key
   float4* beta;     // throughput.xyz, state (depth_left | bounce<<16 | allow<<31)
-  float4* L;        // radiance.xyz, path slot (sample_in_batch * npix + pixel_in_list)
 };
+
+// float4 arrays per path slot: two path streams (3 each), hit, Lout, six NEE
+// job fields; plus two uint32 job words (sj_info, sj_vis).
+constexpr int kSlotF4 = 14;
 
 struct WaveArgs {
   PathStream s[2];  // ping-pong: bounce b reads s[b&1], writes survivors to s[(b&1)^1]
   float4* hit;      // per stream position: t, kind<<28|idx (0 = miss), instance, -
-  float4* Lout;     // per path slot: final radiance.xyz (written when the path ends)
+  float4* Lout;     // per path slot: radiance.xyz, accumulated in place (k_camera zeroes it,
+                    // k_shade adds emission / background, k_nee_apply the direct light)
   // NEE shadow jobs (one per path that samples a light at this bounce), dense
   float4* sj_p;     // shadow origin.xyz, RNG path key
   float4* sj_a;     // area-light shadow dir.xyz, tmax
   float4* sj_h;     // HDRI shadow dir.xyz, -
   uint32_t* sj_info;  // flags (1 area ray, 2 HDRI ray) | bounce << 8
   uint32_t* sj_vis;   // written by k_shadow: bit r set = ray r unoccluded
-  float4* ne_a;     // area-light contribution if visible .xyz, L target
-  float4* ne_h;     // HDRI contribution if visible .xyz
-  float4* ne_beta;  // throughput at the NEE bounce .xyz
+  float4* ne_a;     // area-light contribution if visible .xyz (without HDRI importance
+                    // sampling: already times the throughput), path slot
+  float4* ne_h;     // HDRI contribution if visible .xyz (HDRI importance sampling only)
+  float4* ne_beta;  // throughput at the NEE bounce .xyz (HDRI importance sampling only)
   uint32_t* counts; // queue counters, one 128-B line each (CNT_* below)
   const uint32_t* pixels;   // pixel list (y*W + x) of this call's buckets
   uint32_t npix;
@@ -43,10 +51,6 @@ struct WaveArgs {
   int32_t spill_cap;
   uint32_t slots;   // capacity of every per-slot array (RTG_GUARD bounds checks)
 };
-
-// L target of a NEE record: the survivor's next-stream position, or the
-// path slot (bit 31) when the path ends at this bounce.
-constexpr uint32_t TARGET_SLOT = 0x80000000u;
 
 // Queue counters, each on its own 128-B line (same-line atomics serialise).
 enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT = 96, CNT_FETCH_SH = 128,

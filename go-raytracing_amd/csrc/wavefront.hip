@@ -102,6 +102,7 @@ __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n
   atomicAdd(c + 10, (unsigned long long)n.mat);
   atomicAdd(c + 11, (unsigned long long)n.env);
   atomicAdd(c + 12, (unsigned long long)n.ibox);
+  atomicAdd(c + 13, (unsigned long long)n.spill);
 }
 
 // ---------------------------------------------------------------- camera
@@ -116,10 +117,11 @@ __global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, PathStr
     V3 ro, rd;
     float time;
     get_ray(cam, px, py, key, ro, rd, time);   // GetRay camera.go:368-434
-    stnt(&s.o[i], make_float4(ro.x, ro.y, ro.z, time));
+    (void)time;   // recomputed from the key (ray_time) where needed
+    stnt(&s.o[i], make_float4(ro.x, ro.y, ro.z, asf(i)));
     stnt(&s.d[i], make_float4(rd.x, rd.y, rd.z, asf(key)));
     stnt(&s.beta[i], make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true))));
-    stnt(&s.L[i], make_float4(0.0f, 0.0f, 0.0f, asf(i)));
+    stnt(&a.Lout[i], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
   }
 }
 
@@ -193,8 +195,8 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       p = pn;
       pn = ITEM_NONE;
       if (kCount) cnt.rays++;
-      const int s = trav_init<false, kCount>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), po.w, 0.001f,
-                                             __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
+      const int s = trav_init<false, kCount>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), ray_time(asu(pd.w)),
+                                             0.001f, __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
@@ -275,23 +277,30 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
     const bool live = i < n;
     bool cont = false, want_shadow = false;
     uint32_t slot = 0, key = 0, flags = 0, bounce = 0, nstate = 0;
-    float time = 0.0f, tmax_a = 0.0f;
-    V3 L = mk(0.0f, 0.0f, 0.0f), P = L, sd = L, beta = L, nbeta = L, ca = L, ch = L, da = L, dh = L;
+    float tmax_a = 0.0f;
+    V3 P = mk(0.0f, 0.0f, 0.0f), sd = P, beta = P, nbeta = P, ca = P, ch = P, da = P, dh = P;
+    // L += beta * e on the path's radiance in Lout[slot] (camera.go:466, :481);
+    // adding an exact zero (black background) leaves L unchanged, so it is skipped
+    auto add_L = [&](V3 e) {
+      if (e.x == 0.0f && e.y == 0.0f && e.z == 0.0f) return;
+      float4* lp = &a.Lout[GIX(slot, a.slots, 44)];
+      const float4 l4 = ldnt(lp);
+      const V3 L = add(mk(l4.x, l4.y, l4.z), mul(beta, e));
+      stnt(lp, make_float4(L.x, L.y, L.z, 0.0f));
+    };
     if (live) {
       if (kCount) cnt.rays++;                                    // paths shaded
       const uint32_t ii = GIX(i, a.slots, 41);
-      const float4 h = ldnt(&a.hit[ii]), o4 = ldnt(&cs.o[ii]), d4 = ldnt(&cs.d[ii]), b4 = ldnt(&cs.beta[ii]),
-                   L4 = ldnt(&cs.L[ii]);
+      const float4 h = ldnt(&a.hit[ii]), o4 = ldnt(&cs.o[ii]), d4 = ldnt(&cs.d[ii]), b4 = ldnt(&cs.beta[ii]);
       key = asu(d4.w);
-      slot = asu(L4.w);
+      slot = asu(o4.w);
       const uint32_t st = asu(b4.w);
       const int dleft = int(st & 0xFFFFu);
       bounce = (st >> 16) & 0x7FFFu;
       const bool allow = (st >> 31) != 0u;
       const V3 ro = mk(o4.x, o4.y, o4.z), rd = mk(d4.x, d4.y, d4.z);
-      time = o4.w;
+      const float time = ray_time(key);
       beta = mk(b4.x, b4.y, b4.z);
-      L = mk(L4.x, L4.y, L4.z);
       const uint32_t kh = asu(h.y);
 #ifdef RTG_GUARD
       if (kh == 0xFFFFFFFFu && atomicAdd(&rtg_guard_hits, 1) < 16)
@@ -309,7 +318,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
         } else {
           bg = ld3(cam.background);
         }
-        L = add(L, mul(beta, bg));
+        add_L(bg);
       } else {
         Best b{};
         b.t = h.x; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = int(asu(h.z));
@@ -321,7 +330,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
         V3 att = mk(0.0f, 0.0f, 0.0f);
         bool scat = true, use_mis = false;
         if (m.kind == 4) {                                        // DiffuseLight
-          if (allow) L = add(L, mul(beta, tex_value(sc, m.tex, rec.u, rec.v, rec.P)));
+          if (allow) add_L(tex_value(sc, m.tex, rec.u, rec.v, rec.P));
           scat = false;
         } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
           sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
@@ -437,13 +446,9 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
     block_reserve2(cont, want_shadow, ncount, a.counts + CNT_SHADOW, s_w[par], s_b[par], jc, js);
     if (cont) {
       jc = GIX(jc, a.slots, 43);
-      stnt(&ns.o[jc], make_float4(P.x, P.y, P.z, time));
+      stnt(&ns.o[jc], make_float4(P.x, P.y, P.z, asf(slot)));
       stnt(&ns.d[jc], make_float4(sd.x, sd.y, sd.z, asf(key)));
       stnt(&ns.beta[jc], make_float4(nbeta.x, nbeta.y, nbeta.z, asf(nstate)));
-      stnt(&ns.L[jc], make_float4(L.x, L.y, L.z, asf(slot)));
-    } else if (live) {
-      slot = GIX(slot, a.slots, 44);
-      stnt(&a.Lout[slot], make_float4(L.x, L.y, L.z, 0.0f));
     }
     if (want_shadow) {
       if (kCount) cnt.shadow++;                                  // NEE jobs written
@@ -452,9 +457,15 @@ __global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs
       stnt(&a.sj_a[js], make_float4(da.x, da.y, da.z, tmax_a));
       if (kEnvIS) stnt(&a.sj_h[js], make_float4(dh.x, dh.y, dh.z, 0.0f));
       stnt(&a.sj_info[js], flags | (bounce << 8));
-      stnt(&a.ne_a[js], make_float4(ca.x, ca.y, ca.z, asf(cont ? jc : (slot | TARGET_SLOT))));
-      if (kEnvIS) stnt(&a.ne_h[js], make_float4(ch.x, ch.y, ch.z, 0.0f));
-      stnt(&a.ne_beta[js], make_float4(beta.x, beta.y, beta.z, 0.0f));
+      if (kEnvIS) {
+        stnt(&a.ne_a[js], make_float4(ca.x, ca.y, ca.z, asf(slot)));
+        stnt(&a.ne_h[js], make_float4(ch.x, ch.y, ch.z, 0.0f));
+        stnt(&a.ne_beta[js], make_float4(beta.x, beta.y, beta.z, 0.0f));
+      } else {
+        // only the area ray: L + beta * (0 + ca) = L + beta * ca, bit for bit
+        const V3 bca = mul(beta, ca);
+        stnt(&a.ne_a[js], make_float4(bca.x, bca.y, bca.z, asf(slot)));
+      }
     }
   }
   if (kCount) add_counters(a.counters + KC_SHADE * CNT_BLOCK, cnt, 0);
@@ -544,22 +555,31 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
 }
 
 // ---------------------------------------------------------------- NEE apply
-// L_target += beta_at_bounce * (HDRI contribution if visible + area-light
+// Lout[slot] += beta_at_bounce * (HDRI contribution if visible + area-light
 // contribution if visible), summed in that order (camera.go:549-558).
-__global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count, float4* Lnext) {
+// Without HDRI importance sampling a job carries beta * contribution already;
+// a job whose rays were all occluded adds zero and is skipped.
+template <bool kEnvIS>
+__global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count) {
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
     const uint32_t flags = ldnt(&a.sj_info[k]) & 0xFFu, vis = ldnt(&a.sj_vis[k]);
-    const float4 ea = ldnt(&a.ne_a[k]), pb = ldnt(&a.ne_beta[k]);
-    V3 direct = mk(0.0f, 0.0f, 0.0f);
-    if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
-    if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
-    const uint32_t t = asu(ea.w);
-    float4* Lp = (t & TARGET_SLOT) ? a.Lout + GIX(t & ~TARGET_SLOT, a.slots, 47) : Lnext + GIX(t, a.slots, 48);
-    const float4 L4 = *Lp;
-    const V3 L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
-    *Lp = make_float4(L.x, L.y, L.z, L4.w);
+    if ((flags & vis & 3u) == 0u) continue;
+    const float4 ea = ldnt(&a.ne_a[k]);
+    float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
+    const float4 L4 = ldnt(Lp);
+    V3 L;
+    if (kEnvIS) {
+      const float4 pb = ldnt(&a.ne_beta[k]);
+      V3 direct = mk(0.0f, 0.0f, 0.0f);
+      if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+      if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
+      L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
+    } else {
+      L = add(mk(L4.x, L4.y, L4.z), mk(ea.x, ea.y, ea.z));
+    }
+    stnt(Lp, make_float4(L.x, L.y, L.z, 0.0f));
   }
 }
 
@@ -639,7 +659,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
     const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy>, 256, 0, nslots, cus);
     int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS>, 256, 0, nslots, cus);
     gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;
-    const int gap = grid_for((const void*)k_nee_apply, 256, 0, nslots, cus);
+    const int gap = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
     for (int b = 0; b < plan.max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
 #ifdef RTG_GUARD
@@ -656,7 +676,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
       hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS>), dim3(gsd), dim3(256), 0, st, sc, a, cnt_shadow,
                          fetch_sh, fetch_ext);
       if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_nee_apply, dim3(gap), dim3(256), 0, st, a, cnt_shadow, a.s[nx].L);
+      hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap), dim3(256), 0, st, a, cnt_shadow);
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
         // long-tail scenes (RandomScene depth 50): stop once every path ended
         uint32_t left = 0;

@@ -218,6 +218,7 @@ typedef struct rt_work_counts {
   uint64_t instance_visits, volume_tests;
   uint64_t material_fetches, env_lookups;
   uint64_t instance_box_tests; /* world-space instance culling boxes (32 B)  */
+  uint64_t stack_spills;       /* traversal-stack pushes past the LDS ring (to the global spill area) */
 } rt_work_counts;
 
 /* Summed per-launch durations of the wavefront kernels of the last render

@@ -45,6 +45,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.tri_aux = ptr(h.tri_aux); d.circles = ptr(h.circles); d.circle_rank = ptr(h.circle_rank);
   d.circle_hidx = ptr(h.circle_hidx); d.perlins = ptr(h.perlins); d.images = ptr(h.images);
   d.image_texels = ptr(h.image_texels); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
+  d.inst_entry = ptr(h.inst_entries);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
   d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
   d.tri_rank = ptr(h.tri_rank); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);

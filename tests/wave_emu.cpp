@@ -41,7 +41,7 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
       k_extend<kRing, false, kVol>(sc, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext);
       k_shade<false, kEnvIS, kFancy>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx]);
       k_shadow<kRing, false, kVol, kEnvIS>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
-      k_nee_apply(a, cnt_shadow, a.s[nx].L);
+      k_nee_apply<kEnvIS>(a, cnt_shadow);
     }
     k_accum(a, sb);
   }
@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
   const size_t S = size_t(spb) * npix;
 
   // exactly-sized buffers (the layout of render_wave in api.cpp)
-  std::vector<float4> f4(16 * S, float4{0.0f, 0.0f, 0.0f, 0.0f});
+  std::vector<float4> f4(size_t(kSlotF4) * S, float4{0.0f, 0.0f, 0.0f, 0.0f});
   std::vector<uint32_t> q(CNT_WORDS_Q + 2 * S, 0u);
   std::vector<uint32_t> pixels(npix);
   // bucket-like pixel list: reversed, so slot -> pixel is not the identity
@@ -76,12 +76,12 @@ int main(int argc, char** argv) {
   WaveArgs a{};
   float4* base = f4.data();
   for (int k = 0; k < 2; ++k) {
-    float4* sb = base + size_t(4 * k) * S;
-    a.s[k] = PathStream{sb, sb + S, sb + 2 * S, sb + 3 * S};
+    float4* sb = base + size_t(3 * k) * S;
+    a.s[k] = PathStream{sb, sb + S, sb + 2 * S};
   }
-  a.hit = base + 8 * S; a.Lout = base + 9 * S;
-  a.sj_p = base + 10 * S; a.sj_a = base + 11 * S; a.sj_h = base + 12 * S;
-  a.ne_a = base + 13 * S; a.ne_h = base + 14 * S; a.ne_beta = base + 15 * S;
+  a.hit = base + 6 * S; a.Lout = base + 7 * S;
+  a.sj_p = base + 8 * S; a.sj_a = base + 9 * S; a.sj_h = base + 10 * S;
+  a.ne_a = base + 11 * S; a.ne_h = base + 12 * S; a.ne_beta = base + 13 * S;
   a.counts = q.data();
   a.sj_info = q.data() + CNT_WORDS_Q;
   a.sj_vis = a.sj_info + S;
