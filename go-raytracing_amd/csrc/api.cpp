@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -277,7 +278,11 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   std::memcpy(ctx->pix_pinned, px.data(), npix * sizeof(uint32_t));
   HIPCHK(hipMemcpyAsync(ctx->wpix.p, ctx->pix_pinned, npix * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(ctx->pix_ev, st));
+#ifdef RTG_STAMP
+  HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
+#else
   if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
+#endif
   WaveArgs a{};
   float4* base = static_cast<float4*>(ctx->wstate.p);
   const size_t S = ctx->wslots;
@@ -350,6 +355,23 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   HIPCHK(hipMemcpyAsync(ctx->err_pinned, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(ctx->err_ev, st));
   ctx->err_pending = true;
+#ifdef RTG_STAMP
+  if (!count) {   // diagnostic build: per-kernel segment cycles of the traversal (wave sums)
+    unsigned long long c[CNT_WORDS];
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(c, ctx->counters.p, sizeof c, hipMemcpyDeviceToHost));
+    for (int k : {int(KC_EXTEND), int(KC_SHADOW)}) {
+      const unsigned long long* b = c + k * CNT_BLOCK;
+      const double steps = double(b[20] ? b[20] : 1);
+      fprintf(stderr, "RTG_STAMP %s node-steps %llu cycles/step: load %.1f math %.1f rest %.1f | phase2 total %.3g (%.1f/step)\n",
+              k == KC_EXTEND ? "extend" : "shadow", b[20], b[16] / steps, b[17] / steps, b[18] / steps, double(b[19]),
+              b[19] / steps);
+      const double rounds = double(b[14] ? b[14] : 1);
+      fprintf(stderr, "RTG_STAMP %s phase-2 rounds %llu cycles/round: leaf %.1f inst %.1f inst_end %.1f tail %.1f\n",
+              k == KC_EXTEND ? "extend" : "shadow", b[14], b[21] / rounds, b[22] / rounds, b[23] / rounds, b[15] / rounds);
+    }
+  }
+#endif
   if (count || ms) {
     if ((rc = check_render_error(ctx, true))) return rc;
     if (ms) {
@@ -527,6 +549,8 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(sphere_hidx, sphere_hidx);
   UP(quads, quads);
   UP(quad_hidx, quad_hidx);
+  UP(quad_wref, quad_wref);
+  UP(sphere_wref, sphere_wref);
   UP(tris, tris);
   UP(tri_aux, tri_aux);
   UP(tri_hidx, tri_hidx);

@@ -31,6 +31,12 @@ enum : uint32_t {
   ITEM_INST_END = 3u,   // leave instance: restore the world-space ray
   ITEM_TRI1 = 4u,       // tags 4..7: inline triangle leaf of (tag - 3) triangles
                         // at index.. (no DLeaf fetch: one dependent load less)
+  // World BVH leaves holding ONE top-level object, inline in the node slot
+  // (no DLeaf, no refs fetch: the object's own record is the first load):
+  ITEM_WQUAD = 8u,      // a world quad: index = quad index
+  ITEM_WSPHERE = 9u,    // a world sphere: index = sphere index
+  ITEM_WINST = 10u,     // a world instance: index = ref position; its culling
+                        // box and entry record are one DInstEntry
 };
 constexpr int ITEM_SHIFT = 28;
 constexpr uint32_t ITEM_MASK = (1u << ITEM_SHIFT) - 1u;
@@ -39,9 +45,15 @@ __host__ __device__ inline uint32_t tri_leaf_item(uint32_t first, int n) {
   return ((ITEM_TRI1 + uint32_t(n) - 1u) << ITEM_SHIFT) | first;
 }
 // Leaf-like items (a DLeaf record or an inline triangle leaf).
+__host__ __device__ inline bool item_is_tri_leaf(uint32_t tag) {
+  return tag >= ITEM_TRI1 && tag < ITEM_TRI1 + uint32_t(kInlineTriMax);
+}
+// Leaf-like items (tested in place; the lane carries on with its stack):
+// a DLeaf record, an inline triangle leaf, an inline world quad / sphere.
+// (Instance items are not: they switch the lane's ray.)
 __host__ __device__ inline bool item_is_leaf(uint32_t item) {
   const uint32_t tag = item >> ITEM_SHIFT;
-  return tag == ITEM_LEAF || (tag >= ITEM_TRI1 && tag < ITEM_TRI1 + uint32_t(kInlineTriMax));
+  return tag == ITEM_LEAF || item_is_tri_leaf(tag) || tag == ITEM_WQUAD || tag == ITEM_WSPHERE;
 }
 
 // Primitive reference kinds (leaf "kind" field and ref tags).
@@ -148,23 +160,31 @@ struct alignas(16) DInstance {
   float prm[MAX_WRAP][6];    // translate: off xyz; rot: sin, cos; scale: f xyz, invf xyz
 };
 
-// Instance entry record, one per TLAS ref position (ITEM_INSTANCE items
-// carry the ref position): everything the traversal needs to enter the
-// instance in ONE 128-B line — the wrapper chain's ray-side parameters (the
-// same floats DInstance holds, in the same wrapper order) and the BLAS root
-// item and box — instead of the dependent refs -> DInstance -> DBvh loads.
-// Built from DInstance / DBvh by build_inst_entries (flatten.cpp) after any
-// device BLAS build.  Non-instance refs have nwrap 0 and are never read.
+// Instance entry record, one per TLAS ref position (ITEM_INSTANCE and
+// ITEM_WINST items carry the ref position): everything the traversal needs
+// to cull and enter the instance, with the first three wrappers (Transform
+// .Apply's usual Scale -> RotY -> Translate chain, transform.go:24-46) in the
+// first 128-B line — the world-space culling box (DRefBox), the wrapper
+// chain's ray-side parameters (the same floats DInstance holds, in the same
+// order) and the BLAS root item and box — instead of the dependent
+// leaf -> refs -> culling box -> DInstance -> DBvh loads.  Built from
+// DInstance / DBvh / ref_box by build_inst_entries (flatten.cpp) after any
+// device BLAS build.  Non-instance refs are zero and never read.
 struct alignas(128) DInstEntry {
-  float box[6];              // BLAS root box (object space)
-  uint32_t root_item;
-  int32_t check_box;
-  uint32_t kinds;            // wrapper kind i in bits 4i..4i+3 (outermost first)
-  int32_t nwrap;
-  float prm[MAX_WRAP][3];    // translate: offset; rotate: sin, cos, -; scale: 1/factor
-  float pad[4];
+  float clo[3]; uint32_t kinds;      // culling box lo; wrapper kind i in bits 4i..4i+3 (outermost first)
+  float chi[3]; int32_t nwrap;       // culling box hi
+  float p0[3]; uint32_t root_item;   // wrapper 0 ray-side floats: translate: offset; rotate: sin, cos, -;
+  float p1[3]; int32_t check_box;    //   scale: 1/factor;  BLAS root item, root-box test flag
+  float p2[3]; int32_t pad0;
+  float rlo[3]; int32_t pad1;        // BLAS root box (object space)
+  float rhi[3]; int32_t pad2;
+  float p3[3]; int32_t pad3;
+  float p4[3]; int32_t pad4;         // second line: wrappers 4 and 5 (rare)
+  float p5[3]; int32_t pad5;
+  float pad[24];
 };
-static_assert(sizeof(DInstEntry) == 128, "DInstEntry is one 128-B line");
+static_assert(sizeof(DInstEntry) == 256, "DInstEntry: two 128-B lines");
+static_assert(MAX_WRAP == 6, "DInstEntry holds six wrappers");
 
 struct alignas(16) DVolume {   // volume.go:9-13
   int32_t boundary;          // instance index describing the boundary (chain + list)
@@ -248,6 +268,8 @@ struct DScene {
   const DPlane* planes;
   const DInstance* instances;
   const DInstEntry* inst_entry;  // per TLAS ref position (instance refs)
+  const int32_t* quad_wref;      // per quad: its TLAS ref position if it is a world object (ITEM_WQUAD), else -1
+  const int32_t* sphere_wref;    // per sphere: same (ITEM_WSPHERE)
   const DBvh* blas;
   const DVolume* volumes;
   const DMaterial* materials;

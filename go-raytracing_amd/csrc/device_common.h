@@ -386,7 +386,22 @@ __device__ __forceinline__ bool accept(const DScene& sc, float t, int kind, int 
 // Work counters for the instrumented variant (rt_count_work).
 struct Cnt {
   uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env, ibox, spill;
+#ifdef RTG_STAMP
+  // diagnostic build: s_memtime cycle sums of the traversal's segments, taken
+  // by the first active lane of the wave (so the lane sums are wave sums)
+  uint32_t st_load, st_math, st_rest, st_p2, st_steps, st_leaf, st_inst, st_end, st_tail, st_rounds;
+#endif
 };
+#ifdef RTG_STAMP
+__device__ __forceinline__ uint32_t rtg_stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return uint32_t(t);
+}
+__device__ __forceinline__ bool rtg_lead() { return __lane_id() == uint32_t(__ffsll(__ballot(1)) - 1); }
+#endif
 
 // Volume.Hit (volume.go:34-79) against a boundary given as an instance chain
 // over a list leaf.  ntests = how many times the enclosing leaf calls Hit
@@ -590,6 +605,10 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
+#ifdef RTG_STAMP
+    const bool st_lead = rtg_lead();
+    const uint32_t st0 = rtg_stamp();
+#endif
     // 32-bit byte offsets from the uniform node base (saddr + voffset loads)
     const uint32_t nb = GIX(T.item & ITEM_MASK, sc.n_nodes, 9) << 7;
     const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
@@ -609,6 +628,10 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));
 #endif
     if (kCount) cnt.nodes++;
+#ifdef RTG_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t st1 = rtg_stamp();
+#endif
     const float hi = kAny ? T.tmax : best.t;
     const float inf = __builtin_inff();
     auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
@@ -632,6 +655,9 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
     };
     cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2);
+#ifdef RTG_STAMP
+    const uint32_t st2 = rtg_stamp();
+#endif
     if (!(t0 < inf)) {
       T.item = pop();
     } else {
@@ -648,12 +674,26 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
+#ifdef RTG_STAMP
+    if (st_lead) {
+      const uint32_t st3 = rtg_stamp();
+      cnt.st_load += st1 - st0; cnt.st_math += st2 - st1; cnt.st_rest += st3 - st2; cnt.st_steps++;
+    }
+#endif
     if (!__any(T.lf == ITEM_NONE)) break;   // every lane holds a postponed item
   }
   // ---------------- phase 2: leaves, instance entry / exit
+#ifdef RTG_STAMP
+  const bool st_lead2 = rtg_lead();
+  const uint32_t st4 = rtg_stamp();
+#endif
   while (T.lf != ITEM_NONE) {
+#ifdef RTG_STAMP
+    const bool st_l = rtg_lead();
+    const uint32_t sa = rtg_stamp();
+#endif
     const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
-    if (tag == ITEM_LEAF || tag >= ITEM_TRI1) {
+    if (tag == ITEM_LEAF || item_is_tri_leaf(tag)) {
       DLeaf leaf;
       if (tag == ITEM_LEAF) leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
       else { leaf.first = idx; leaf.info = make_leaf_info(int(tag - ITEM_TRI1) + 1, PK_TRI, 1); }
@@ -701,71 +741,133 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           best.refpos = refpos; best.primpos = primpos;
         }
       }
-    } else if (tag == ITEM_INSTANCE) {
-      // one 128-B entry record per instance ref (DInstEntry): the wrapper
-      // chain's ray-side floats and the BLAS root in one line, instead of the
-      // dependent refs -> DInstance -> DBvh loads.  The any-hit kernel loads
-      // it as five float4s issued together; the closest-hit kernel, whose
-      // registers are tighter (the hit record), field by field (measured:
-      // each form is the faster one in its kernel).
+    } else if (tag == ITEM_WQUAD || tag == ITEM_WSPHERE) {
+      // a world leaf of one quad / sphere, inline in its node slot
+      float t = 0.0f;
+      bool ok;
+      int pk;
+      if (tag == ITEM_WQUAD) {
+        pk = PK_QUAD;
+        if (kCount) cnt.quad++;
+        ok = quad_t(sc.quads[GIX(idx, sc.n_quads, 37)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
+      } else {
+        pk = PK_SPHERE;
+        if (kCount) cnt.sph++;
+        ok = sphere_t(sc.spheres[GIX(idx, sc.n_spheres, 38)], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+      }
+      if (ok) {
+        if (kAny) return TRAV_ANYHIT;
+        const int refpos = pk == PK_QUAD ? sc.quad_wref[GIX(idx, sc.n_quads, 39)] : sc.sphere_wref[GIX(idx, sc.n_spheres, 49)];
+        if (accept(sc, t, pk, refpos, 0, best)) {
+          best.t = t; best.kind = pk; best.idx = int(idx);
+          best.refpos = refpos; best.primpos = 0;
+        }
+      }
+    } else if (tag == ITEM_INSTANCE || tag == ITEM_WINST) {
+      // One entry record per instance ref (DInstEntry): for a world leaf of
+      // one instance (ITEM_WINST) first the world-space cull on the
+      // instance's own padded bbox (an ITEM_INSTANCE from a leaf of several
+      // objects was culled there), then the wrapper chain (the ray into
+      // object space, transform.go) and the BLAS root: one line instead of
+      // the dependent leaf -> refs -> culling box -> DInstance -> DBvh loads.
+      // The any-hit kernel loads the line as five float4s issued together;
+      // the closest-hit kernel, whose registers are tighter (the hit
+      // record), field by field (each form measured the faster in its kernel).
+      const bool winst = tag == ITEM_WINST;
+      const float hi = kAny ? T.tmax : best.t;
+      float tn = 0.0f;
       if constexpr (!kAny) {
         const DInstEntry& E = sc.inst_entry[GIX(idx, sc.n_refs, 17)];
-        if (kCount) cnt.inst++;
-        V3 o = S.wo(), d = S.wd();
-        const uint32_t kinds = E.kinds;
-        const int nwrap = E.nwrap;
-        for (int i = 0; i < nwrap; ++i) wrap_ray3(int((kinds >> (4 * i)) & 15u), E.prm[i][0], E.prm[i][1], E.prm[i][2], o, d);
-        const TRay orr = make_tray(o, d);
-        bool enter = true;
-        float tn = 0.0f;
-        if (E.check_box)   // BVHNode.Hit tests its own bbox first
-          enter = box_hit(E.box[0], E.box[1], E.box[2], E.box[3], E.box[4], E.box[5], orr, T.tmin, best.t, tn);
-        if (enter) {
-          if (T.item < ITEM_POP) push(T.item);
-          push(ITEM_INST_END << ITEM_SHIFT);
-          T.cr = orr; T.cur_ref = int(idx);
-          T.item = E.root_item;
+        bool go = true;
+        if (winst) {
+          if (kCount) cnt.ibox++;
+          go = box_hit(E.clo[0], E.chi[0], E.clo[1], E.chi[1], E.clo[2], E.chi[2], T.cr, T.tmin, hi, tn);
+        }
+        if (go) {
+          if (kCount) cnt.inst++;
+          V3 o = S.wo(), d = S.wd();
+          const uint32_t kinds = E.kinds;
+          const int nwrap = E.nwrap;
+          auto wr = [&](int i, const float* q) {
+            if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), q[0], q[1], q[2], o, d);
+          };
+          wr(0, E.p0); wr(1, E.p1); wr(2, E.p2);
+          if (nwrap > 3) { wr(3, E.p3); wr(4, E.p4); wr(5, E.p5); }
+          const TRay orr = make_tray(o, d);
+          bool enter = true;
+          if (E.check_box)   // BVHNode.Hit tests its own bbox first
+            enter = box_hit(E.rlo[0], E.rhi[0], E.rlo[1], E.rhi[1], E.rlo[2], E.rhi[2], orr, T.tmin, hi, tn);
+          if (enter) {
+            if (T.item < ITEM_POP) push(T.item);
+            push(ITEM_INST_END << ITEM_SHIFT);
+            T.cr = orr; T.cur_ref = int(idx);
+            T.item = E.root_item;
+          }
         }
       } else {
         const float4* e4 = reinterpret_cast<const float4*>(sc.inst_entry + GIX(idx, sc.n_refs, 17));
-        const float4 h0 = e4[0], h1 = e4[1], h2 = e4[2], q3 = e4[3], q4 = e4[4];
-        if (kCount) cnt.inst++;
-        const uint32_t kinds = __float_as_uint(h2.x);
-        const int nwrap = int(__float_as_uint(h2.y));
-        V3 o = S.wo(), d = S.wd();
-        auto wr = [&](int i, float a, float b, float c) {
-          if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), a, b, c, o, d);
-        };
-        wr(0, h2.z, h2.w, q3.x);
-        wr(1, q3.y, q3.z, q3.w);
-        wr(2, q4.x, q4.y, q4.z);
-        if (nwrap > 3) {
-          const float4 q5 = e4[5], q6 = e4[6];
-          wr(3, q4.w, q5.x, q5.y);
-          wr(4, q5.z, q5.w, q6.x);
-          wr(5, q6.y, q6.z, q6.w);
+        const float4 c0 = e4[0], c1 = e4[1], q0 = e4[2], q1 = e4[3], q2 = e4[4];
+        bool go = true;
+        if (winst) {
+          if (kCount) cnt.ibox++;
+          go = box_hit(c0.x, c1.x, c0.y, c1.y, c0.z, c1.z, T.cr, T.tmin, hi, tn);
         }
-        const TRay orr = make_tray(o, d);
-        bool enter = true;
-        float tn = 0.0f;
-        if (__float_as_uint(h1.w) != 0u)   // check_box: BVHNode.Hit tests its own bbox first
-          enter = box_hit(h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, orr, T.tmin, T.tmax, tn);
-        if (enter) {
-          if (T.item < ITEM_POP) push(T.item);
-          push(ITEM_INST_END << ITEM_SHIFT);
-          T.cr = orr; T.cur_ref = int(idx);
-          T.item = __float_as_uint(h1.z);   // BLAS root item
+        if (go) {
+          if (kCount) cnt.inst++;
+          const uint32_t kinds = __float_as_uint(c0.w);
+          const int nwrap = int(__float_as_uint(c1.w));
+          V3 o = S.wo(), d = S.wd();
+          auto wr = [&](int i, float a, float b, float c) {
+            if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), a, b, c, o, d);
+          };
+          wr(0, q0.x, q0.y, q0.z);
+          wr(1, q1.x, q1.y, q1.z);
+          wr(2, q2.x, q2.y, q2.z);
+          if (nwrap > 3) {
+            const float4 q3 = e4[7], q4 = e4[8], q5 = e4[9];
+            wr(3, q3.x, q3.y, q3.z);
+            wr(4, q4.x, q4.y, q4.z);
+            wr(5, q5.x, q5.y, q5.z);
+          }
+          const TRay orr = make_tray(o, d);
+          bool enter = true;
+          if (__float_as_uint(q1.w) != 0u) {   // check_box: BVHNode.Hit tests its own bbox first
+            const float4 r0 = e4[5], r1 = e4[6];
+            enter = box_hit(r0.x, r1.x, r0.y, r1.y, r0.z, r1.z, orr, T.tmin, hi, tn);
+          }
+          if (enter) {
+            if (T.item < ITEM_POP) push(T.item);
+            push(ITEM_INST_END << ITEM_SHIFT);
+            T.cr = orr; T.cur_ref = int(idx);
+            T.item = __float_as_uint(q0.w);   // BLAS root item
+          }
         }
       }
     } else {  // ITEM_INST_END: back to the world-space ray
       T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
     }
+#ifdef RTG_STAMP
+    const uint32_t sb = rtg_stamp();
+#endif
     T.lf = ITEM_NONE;
     // ITEM_NONE here only means the stack was empty when this lane last
     // popped; the leaf just processed may have pushed instance items since.
     if (T.item == ITEM_POP || T.item == ITEM_NONE) T.item = pop();
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE) postpone();
+#ifdef RTG_STAMP
+    if (st_l) {
+      const uint32_t se = rtg_stamp();
+      const uint32_t body = sb - sa;
+      if (tag == ITEM_INSTANCE || tag == ITEM_WINST) cnt.st_inst += body;
+      else if (tag == ITEM_INST_END) cnt.st_end += body;
+      else cnt.st_leaf += body;
+      cnt.st_tail += se - sb; cnt.st_rounds++;
+    }
+#endif
   }
+#ifdef RTG_STAMP
+  if (st_lead2) cnt.st_p2 += rtg_stamp() - st4;
+#endif
   return (T.item == ITEM_NONE && T.lf == ITEM_NONE) ? TRAV_DONE : TRAV_RUNNING;
 }
 

@@ -1048,6 +1048,7 @@ struct Flattener {
     int n = 0;
     S.tlas.root_item = collapse4(S.tlas.root_item, n);
     S.tlas_need4 = n;
+    const size_t n_tlas4 = S.nodes4.size();   // the world BVH's nodes come first
     S.blas_need4 = 0;
     for (DBvh& b : S.blas) {
       b.root_item = collapse4(b.root_item, n);
@@ -1057,6 +1058,25 @@ struct Flattener {
     // first index + count; BLAS roots keep their DLeaf, volumes read it).
     for (DNode4& o : S.nodes4)
       for (uint32_t& it : o.item) it = inline_leaf(it);
+    // World leaves of one quad / sphere / instance become inline items too.
+    S.quad_wref.assign(S.quads.size(), -1);
+    S.sphere_wref.assign(S.spheres.size(), -1);
+    for (size_t i = 0; i < n_tlas4; ++i)
+      for (uint32_t& it : S.nodes4[i].item) it = inline_world_leaf(it);
+  }
+  uint32_t inline_world_leaf(uint32_t item) {
+    if ((item >> ITEM_SHIFT) != ITEM_LEAF || item == empty_leaf) return item;
+    const DLeaf& L = S.leaves[item & ITEM_MASK];
+    // a repeated test (ntests 2, the BVHNode{leaf,leaf} wrapper) of a quad,
+    // sphere or instance finds the same hit: only volumes need the count
+    if (leaf_kind(L.info) != PK_MIXED || leaf_count(L.info) != 1) return item;
+    const uint32_t ref = S.refs[L.first];
+    const int kind = int(ref >> REF_SHIFT);
+    const uint32_t idx = ref & REF_MASK;
+    if (kind == PK_QUAD) { S.quad_wref[idx] = int32_t(L.first); return (ITEM_WQUAD << ITEM_SHIFT) | idx; }
+    if (kind == PK_SPHERE) { S.sphere_wref[idx] = int32_t(L.first); return (ITEM_WSPHERE << ITEM_SHIFT) | idx; }
+    if (kind == PK_INSTANCE) return (ITEM_WINST << ITEM_SHIFT) | L.first;
+    return item;
   }
   uint32_t inline_leaf(uint32_t item) const {
     if ((item >> ITEM_SHIFT) != ITEM_LEAF || item == empty_leaf) return item;
@@ -1135,8 +1155,13 @@ void build_inst_entries(HostScene& S) {
     if (int(S.refs[r] >> REF_SHIFT) != PK_INSTANCE) continue;
     const DInstance& in = S.instances[S.refs[r] & REF_MASK];
     const DBvh& bb = S.blas[size_t(in.blas)];
+    const DRefBox& cb = S.ref_box[r];
     DInstEntry& e = S.inst_entries[r];
-    for (int k = 0; k < 6; ++k) e.box[k] = bb.box[k];
+    float* prm[MAX_WRAP] = {e.p0, e.p1, e.p2, e.p3, e.p4, e.p5};
+    for (int a = 0; a < 3; ++a) {
+      e.clo[a] = cb.lo[a]; e.chi[a] = cb.hi[a];
+      e.rlo[a] = bb.box[2 * a]; e.rhi[a] = bb.box[2 * a + 1];
+    }
     e.root_item = bb.root_item;
     e.check_box = bb.check_box;
     e.nwrap = in.nwrap;
@@ -1146,7 +1171,7 @@ void build_inst_entries(HostScene& S) {
       // the floats wrap_ray reads (device_common.h): translate p[0..2],
       // rotations p[0] (sin), p[1] (cos), scale p[3..5] (1/factor)
       const int o = in.kind[i] == W_SCALE ? 3 : 0;
-      for (int j = 0; j < 3; ++j) e.prm[i][j] = in.prm[i][o + j];
+      for (int j = 0; j < 3; ++j) prm[i][j] = in.prm[i][o + j];
     }
   }
 }

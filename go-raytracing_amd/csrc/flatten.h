@@ -35,6 +35,7 @@ struct HostScene {
   std::vector<int32_t> plane_hidx;
   std::vector<DInstance> instances;
   std::vector<DInstEntry> inst_entries;   // per ref (build_inst_entries)
+  std::vector<int32_t> quad_wref, sphere_wref;   // per prim: world ref position (inline world leaves) or -1
   std::vector<DBvh> blas;
   std::vector<DVolume> volumes;
   std::vector<int32_t> volume_hidx;

@@ -79,7 +79,7 @@ struct WavePlan {
 
 enum : uint8_t { KC_EXTEND = 0, KC_SHADE = 1, KC_SHADOW = 2, KC_OTHER = 3 };
 // Counter blocks (16 x u64 each): one per kernel class.
-constexpr int CNT_BLOCK = 16;
+constexpr int CNT_BLOCK = 24;
 
 hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs& a, const WavePlan& plan, int stack,
                             bool count, float* out, int accumulate, hipStream_t st);

@@ -103,6 +103,18 @@ __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n
   atomicAdd(c + 11, (unsigned long long)n.env);
   atomicAdd(c + 12, (unsigned long long)n.ibox);
   atomicAdd(c + 13, (unsigned long long)n.spill);
+#ifdef RTG_STAMP
+  atomicAdd(c + 16, (unsigned long long)n.st_load);
+  atomicAdd(c + 17, (unsigned long long)n.st_math);
+  atomicAdd(c + 18, (unsigned long long)n.st_rest);
+  atomicAdd(c + 19, (unsigned long long)n.st_p2);
+  atomicAdd(c + 20, (unsigned long long)n.st_steps);
+  atomicAdd(c + 21, (unsigned long long)n.st_leaf);
+  atomicAdd(c + 22, (unsigned long long)n.st_inst);
+  atomicAdd(c + 23, (unsigned long long)n.st_end);
+  atomicAdd(c + 15, (unsigned long long)n.st_tail);
+  atomicAdd(c + 14, (unsigned long long)n.st_rounds);
+#endif
 }
 
 // ---------------------------------------------------------------- camera
@@ -215,7 +227,11 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
     }
   }
+#ifdef RTG_STAMP
+  add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
+#else
   if (kCount) add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
+#endif
 }
 
 // ---------------------------------------------------------------- shade
@@ -245,8 +261,11 @@ __device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, u
 // compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 
+#ifndef RTG_SHADE_WAVES
+#define RTG_SHADE_WAVES 1
+#endif
 template <bool kCount, bool kEnvIS, bool kFancy>
-__global__ __launch_bounds__(256) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+__global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                const uint32_t* count, PathStream ns, uint32_t* ncount) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
   // sit on every path's dependent-load chain (hit -> material -> texture,
@@ -551,7 +570,11 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
   }
+#ifdef RTG_STAMP
+  add_counters(a.counters + KC_SHADOW * CNT_BLOCK, cnt, 0);
+#else
   if (kCount) add_counters(a.counters + KC_SHADOW * CNT_BLOCK, cnt, 0);
+#endif
 }
 
 // ---------------------------------------------------------------- NEE apply

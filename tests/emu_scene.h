@@ -46,6 +46,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.circle_hidx = ptr(h.circle_hidx); d.perlins = ptr(h.perlins); d.images = ptr(h.images);
   d.image_texels = ptr(h.image_texels); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
   d.inst_entry = ptr(h.inst_entries);
+  d.quad_wref = ptr(h.quad_wref); d.sphere_wref = ptr(h.sphere_wref);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
   d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
   d.tri_rank = ptr(h.tri_rank); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);

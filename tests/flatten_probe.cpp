@@ -26,8 +26,18 @@ static void check_item(const HostScene& S, uint32_t it, const char* where) {
   const uint32_t tag = it >> ITEM_SHIFT, idx = it & ITEM_MASK;
   if (tag == ITEM_NODE) CHECK(idx < S.nodes4.size(), std::string(where) + ": node item out of range");
   else if (tag == ITEM_LEAF) CHECK(idx < S.leaves.size(), std::string(where) + ": leaf item out of range");
-  else if (item_is_leaf(it))
+  else if (item_is_tri_leaf(tag))
     CHECK(size_t(idx) + (tag - ITEM_TRI1) + 1 <= S.tris.size(), std::string(where) + ": inline triangle leaf out of range");
+  else if (tag == ITEM_WQUAD)
+    CHECK(idx < S.quads.size() && S.quad_wref[idx] >= 0 && size_t(S.quad_wref[idx]) < S.refs.size() &&
+              S.refs[size_t(S.quad_wref[idx])] == ((uint32_t(PK_QUAD) << REF_SHIFT) | idx),
+          std::string(where) + ": inline world quad");
+  else if (tag == ITEM_WSPHERE)
+    CHECK(idx < S.spheres.size() && S.sphere_wref[idx] >= 0 && size_t(S.sphere_wref[idx]) < S.refs.size() &&
+              S.refs[size_t(S.sphere_wref[idx])] == ((uint32_t(PK_SPHERE) << REF_SHIFT) | idx),
+          std::string(where) + ": inline world sphere");
+  else if (tag == ITEM_WINST)
+    CHECK(idx < S.refs.size() && int(S.refs[idx] >> REF_SHIFT) == PK_INSTANCE, std::string(where) + ": inline world instance");
   else CHECK(false, std::string(where) + ": bad item tag");
 }
 
@@ -65,16 +75,24 @@ int main(int argc, char** argv) {
   // it was collapsed from (non-empty child slots only), and every child box
   // of a BVH4 node contains the boxes inside that child.
   {
-    std::vector<int> seen(S.leaves.size(), 0), seen_tri(S.tris.size(), 0);
+    std::vector<int> seen(S.leaves.size(), 0), seen_tri(S.tris.size(), 0), seen_ref(S.refs.size(), 0);
     std::vector<uint32_t> st;
     auto walk = [&](uint32_t root) {
       st.assign(1, root);
       while (!st.empty()) {
         const uint32_t it = st.back();
         st.pop_back();
-        if ((it >> ITEM_SHIFT) == ITEM_LEAF) { seen[it & ITEM_MASK]++; continue; }
-        if (item_is_leaf(it)) {   // inline triangle leaf
-          if ((it & ITEM_MASK) < S.tris.size()) seen_tri[it & ITEM_MASK]++;
+        const uint32_t tg = it >> ITEM_SHIFT, ix = it & ITEM_MASK;
+        if (tg == ITEM_LEAF) { seen[ix]++; continue; }
+        if (item_is_tri_leaf(tg)) {   // inline triangle leaf
+          if (ix < S.tris.size()) seen_tri[ix]++;
+          continue;
+        }
+        // inline world leaves of one object: the ref position they stand for
+        if (tg == ITEM_WINST && ix < S.refs.size()) { seen_ref[ix]++; continue; }
+        if (tg == ITEM_WQUAD && ix < S.quads.size() && S.quad_wref[ix] >= 0) { seen_ref[size_t(S.quad_wref[ix])]++; continue; }
+        if (tg == ITEM_WSPHERE && ix < S.spheres.size() && S.sphere_wref[ix] >= 0) {
+          seen_ref[size_t(S.sphere_wref[ix])]++;
           continue;
         }
         if ((it >> ITEM_SHIFT) != ITEM_NODE || (it & ITEM_MASK) >= S.nodes4.size()) continue;
@@ -100,7 +118,9 @@ int main(int argc, char** argv) {
       for (uint32_t it : {n.litem, n.ritem})
         if ((it >> ITEM_SHIFT) == ITEM_LEAF && (it & ITEM_MASK) != 0u) {
           const DLeaf& L = S.leaves[it & ITEM_MASK];
-          const bool inl = leaf_kind(L.info) == PK_TRI && L.first < S.tris.size() && seen_tri[L.first] > 0;
+          const bool inl = (leaf_kind(L.info) == PK_TRI && L.first < S.tris.size() && seen_tri[L.first] > 0) ||
+                           (leaf_kind(L.info) == PK_MIXED && leaf_count(L.info) == 1 && L.first < S.refs.size() &&
+                            seen_ref[L.first] > 0);
           CHECK(seen[it & ITEM_MASK] > 0 || inl, "BVH2 leaf not reached through the BVH4");
         }
   }
@@ -133,6 +153,25 @@ int main(int argc, char** argv) {
   for (const DInstance& in : S.instances) {
     CHECK(in.blas >= 0 && size_t(in.blas) < S.blas.size(), "instance blas");
     CHECK(in.nwrap >= 0 && in.nwrap <= MAX_WRAP, "instance nwrap");
+  }
+  // instance entry records mirror DInstance / DBvh / the culling box
+  CHECK(S.inst_entries.size() == S.refs.size(), "one entry record per ref");
+  for (size_t r = 0; r < S.refs.size() && r < S.inst_entries.size(); ++r) {
+    if (int(S.refs[r] >> REF_SHIFT) != PK_INSTANCE) continue;
+    const DInstance& in = S.instances[S.refs[r] & REF_MASK];
+    const DInstEntry& e = S.inst_entries[r];
+    const DBvh& bb = S.blas[size_t(in.blas)];
+    CHECK(e.nwrap == in.nwrap && e.root_item == bb.root_item && e.check_box == bb.check_box, "entry header");
+    const float* prm[MAX_WRAP] = {e.p0, e.p1, e.p2, e.p3, e.p4, e.p5};
+    for (int i = 0; i < in.nwrap; ++i) {
+      CHECK(int((e.kinds >> (4 * i)) & 15u) == in.kind[i], "entry wrapper kind");
+      const int o = in.kind[i] == W_SCALE ? 3 : 0;
+      for (int j = 0; j < 3; ++j) CHECK(prm[i][j] == in.prm[i][o + j], "entry wrapper floats");
+    }
+    for (int a = 0; a < 3; ++a)
+      CHECK(e.clo[a] == S.ref_box[r].lo[a] && e.chi[a] == S.ref_box[r].hi[a] && e.rlo[a] == bb.box[2 * a] &&
+                e.rhi[a] == bb.box[2 * a + 1],
+            "entry boxes");
   }
   for (const DVolume& v : S.volumes) CHECK(v.boundary >= 0 && size_t(v.boundary) < S.instances.size(), "volume boundary");
   for (const DMaterial& m : S.materials) CHECK(m.tex < int(S.textures.size()), "material texture");
