@@ -473,6 +473,14 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
 // ----------------------------------------------------------------------------
 constexpr uint32_t ITEM_NONE = 0xFFFFFFFFu;
+// RTG_WIDE_CLOSEST: the closest-hit traversal also issues its leaf and
+// instance-record loads together (as the any-hit one does) — it needs the
+// registers of a lower occupancy (tuning knob).
+#ifdef RTG_WIDE_CLOSEST
+constexpr bool kWideClosest = true;
+#else
+constexpr bool kWideClosest = false;
+#endif
 constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the stack"
 
 // Per-lane traversal stack: a ring of `cap` (power of two) entries in LDS,
@@ -483,14 +491,21 @@ constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the sta
 // The lane's world-space ray (origin, direction, 1/direction) lives beside it
 // in LDS: it is read only on instance entry / exit and volume tests, so it
 // need not occupy nine VGPRs for the whole traversal.
+// Only `lds` is per lane (one VGPR); the rest is block-uniform: the lane's
+// spill column is spill_blk + (its LDS slot - lds0), formed on the rare
+// spill path, and the world ray sits at lds + cap * stride.
 struct TStack {
   uint32_t* lds;       // this lane's slot 0
   int stride;          // LDS words between slots (lanes interleaved)
   int cap;             // LDS entries (power of two)
-  uint32_t* spill;     // this lane's spill entry 0 (nullptr: spill_cap == 0)
+  uint32_t* spill_blk; // this block's spill column 0 (nullptr: spill_cap == 0)
+  const uint32_t* lds0;  // the block's slot-0 row (lane = lds - lds0)
   int sstride;         // words between spill entries
   int spill_cap;
-  float* wr;           // this lane's world ray: 9 floats, `stride` apart
+  __device__ __forceinline__ float* wrp() const { return reinterpret_cast<float*>(lds + cap * stride); }
+  __device__ __forceinline__ uint32_t* spill_at(int k) const {
+    return spill_blk + (lds - lds0) + size_t(GIX(k, spill_cap, 25)) * sstride;
+  }
 #ifdef RTG_WORLD_RAY_REGS
   mutable V3 wo_, wd_, winv_;
   __device__ __forceinline__ void save_world(V3 o, V3 d, V3 inv) const { wo_ = o; wd_ = d; winv_ = inv; }
@@ -499,29 +514,36 @@ struct TStack {
   __device__ __forceinline__ V3 winv() const { return winv_; }
 #else
   __device__ __forceinline__ void save_world(V3 o, V3 d, V3 inv) const {
+    float* wr = wrp();
     wr[0] = o.x; wr[stride] = o.y; wr[2 * stride] = o.z;
     wr[3 * stride] = d.x; wr[4 * stride] = d.y; wr[5 * stride] = d.z;
     wr[6 * stride] = inv.x; wr[7 * stride] = inv.y; wr[8 * stride] = inv.z;
   }
-  __device__ __forceinline__ V3 wo() const { return mk(wr[0], wr[stride], wr[2 * stride]); }
-  __device__ __forceinline__ V3 wd() const { return mk(wr[3 * stride], wr[4 * stride], wr[5 * stride]); }
-  __device__ __forceinline__ V3 winv() const { return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]); }
+  __device__ __forceinline__ V3 wo() const { const float* wr = wrp(); return mk(wr[0], wr[stride], wr[2 * stride]); }
+  __device__ __forceinline__ V3 wd() const {
+    const float* wr = wrp();
+    return mk(wr[3 * stride], wr[4 * stride], wr[5 * stride]);
+  }
+  __device__ __forceinline__ V3 winv() const {
+    const float* wr = wrp();
+    return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]);
+  }
 #endif
   __device__ __forceinline__ void push(int sp, uint32_t v) const {
     uint32_t* slot = lds + (sp & (cap - 1)) * stride;
-    if (sp >= cap) spill[size_t(GIX(sp - cap, spill_cap, 25)) * sstride] = *slot;
+    if (sp >= cap) *spill_at(sp - cap) = *slot;
     *slot = v;
   }
   __device__ __forceinline__ uint32_t pop(int sp) const {   // sp = new depth
     uint32_t* slot = lds + (sp & (cap - 1)) * stride;
     const uint32_t v = *slot;
-    if (sp >= cap) *slot = spill[size_t(GIX(sp - cap, spill_cap, 26)) * sstride];
+    if (sp >= cap) *slot = *spill_at(sp - cap);
     return v;
   }
 };
 // LDS words per lane: `cap` stack entries + the 9-float world ray.
 __device__ __forceinline__ TStack lds_stack_only(uint32_t* lds, int stride, int cap) {
-  return TStack{lds, stride, cap, nullptr, 0, 0, reinterpret_cast<float*>(lds + cap * stride)};
+  return TStack{lds, stride, cap, nullptr, lds, 0, 0};
 }
 
 // Resumable traversal state (one lane, one ray).
@@ -693,10 +715,47 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const uint32_t sa = rtg_stamp();
 #endif
     const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
-    if (tag == ITEM_LEAF || item_is_tri_leaf(tag)) {
-      DLeaf leaf;
-      if (tag == ITEM_LEAF) leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
-      else { leaf.first = idx; leaf.info = make_leaf_info(int(tag - ITEM_TRI1) + 1, PK_TRI, 1); }
+    if (item_is_tri_leaf(tag)) {
+      // inline triangle leaf (BLAS, tested once; the host SAH builder's
+      // leaves hold <= 2): any-hit rays take the triangles two at a time, both
+      // loads issued before either test (the second index repeats the first
+      // when there is none); measured the faster form in each kernel
+      const int n = int(tag - ITEM_TRI1) + 1;
+      const bool world = T.cur_ref < 0;
+      if constexpr (kAny || kWideClosest) {   // both loads of a pair issued before either test
+        for (int k = 0; k < n; k += 2) {
+          const uint32_t pa = idx + uint32_t(k), pb = k + 1 < n ? pa + 1u : pa;
+          const DTri ta = sc.tris[GIX(pa, sc.n_tris, 12)], tb = sc.tris[GIX(pb, sc.n_tris, 12)];
+          for (int j = 0; j < 2 && k + j < n; ++j) {
+            float t = 0.0f;
+            if (kCount) cnt.tri++;
+            if (!tri_t(j ? tb : ta, T.cr.o, T.cr.d, T.tmin, t)) continue;
+            if (kAny) { if (t <= T.tmax) return TRAV_ANYHIT; continue; }
+            const int pos = int(pa) + j;
+            const int refpos = world ? pos : T.cur_ref;
+            const int primpos = world ? 0 : (PRIM_IN_INST | pos);
+            if (accept(sc, t, PK_TRI, refpos, primpos, best)) {
+              best.t = t; best.kind = PK_TRI; best.idx = pos;
+              best.refpos = refpos; best.primpos = primpos;
+            }
+          }
+        }
+      } else {   // closest hit: one triangle at a time (a pair spills registers here)
+        for (int k = 0; k < n; ++k) {
+          const int pos = int(idx) + k;
+          float t = 0.0f;
+          if (kCount) cnt.tri++;
+          if (!tri_t(sc.tris[GIX(pos, sc.n_tris, 12)], T.cr.o, T.cr.d, T.tmin, t)) continue;
+          const int refpos = world ? pos : T.cur_ref;
+          const int primpos = world ? 0 : (PRIM_IN_INST | pos);
+          if (accept(sc, t, PK_TRI, refpos, primpos, best)) {
+            best.t = t; best.kind = PK_TRI; best.idx = pos;
+            best.refpos = refpos; best.primpos = primpos;
+          }
+        }
+      }
+    } else if (tag == ITEM_LEAF) {
+      const DLeaf leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
       const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
       const bool world = T.cur_ref < 0;
       for (int k = 0; k < n; ++k) {
@@ -776,7 +835,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const bool winst = tag == ITEM_WINST;
       const float hi = kAny ? T.tmax : best.t;
       float tn = 0.0f;
-      if constexpr (!kAny) {
+      if constexpr (!kAny && !kWideClosest) {
         const DInstEntry& E = sc.inst_entry[GIX(idx, sc.n_refs, 17)];
         bool go = true;
         if (winst) {

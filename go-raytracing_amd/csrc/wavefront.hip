@@ -193,9 +193,8 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
   if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
-  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap,
-                 reinterpret_cast<float*>(lds_stack + STACK * 256 + threadIdx.x)};
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
+                 a.spill_cap};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool P{0u, 0u, false};
@@ -502,9 +501,8 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
-  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + lane, int(a.spill_lanes), a.spill_cap,
-                 reinterpret_cast<float*>(lds_stack + STACK * 256 + threadIdx.x)};
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
+                 a.spill_cap};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool Q{0u, 0u, false};
