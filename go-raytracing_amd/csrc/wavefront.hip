@@ -3,8 +3,8 @@
 // same reference functions as device_common.h (camera.go:368-678 et al.).
 //
 // Per batch of path slots (slot = sample_in_batch * npix + pixel_in_list):
-//   k_camera    : GetRay (camera.go:368-388) for every slot -> stream 0
-//   repeat max_depth times (stream s = bounce & 1):
+//   repeat max_depth times (stream s = bounce & 1; bounce 0 has no stream:
+//   its kernels regenerate each slot's camera ray, GetRay camera.go:368-434):
 //     k_extend    : closest hit (BVHNode.Hit ... bvh.go:219-239) for every
 //                   path of stream s; persistent waves claim runs of stream
 //                   positions (one atomic per run) and prefetch the next ray
@@ -118,23 +118,19 @@ __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n
 }
 
 // ---------------------------------------------------------------- camera
-__global__ __launch_bounds__(256) void k_camera(DCamera cam, WaveArgs a, PathStream s, uint32_t nslots,
-                                                uint32_t sample_base) {
-  const uint32_t gs = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += gs) {
-    const uint32_t sm = i / a.npix, pi = i - sm * a.npix;
-    const uint32_t pix = a.pixels[pi];
-    const int px = int(pix % uint32_t(cam.width)), py = int(pix / uint32_t(cam.width));
-    const uint32_t key = path_key(a.seed, pix, sample_base + sm);
-    V3 ro, rd;
-    float time;
-    get_ray(cam, px, py, key, ro, rd, time);   // GetRay camera.go:368-434
-    (void)time;   // recomputed from the key (ray_time) where needed
-    stnt(&s.o[i], make_float4(ro.x, ro.y, ro.z, asf(i)));
-    stnt(&s.d[i], make_float4(rd.x, rd.y, rd.z, asf(key)));
-    stnt(&s.beta[i], make_float4(1.0f, 1.0f, 1.0f, asf(pack_state(a.max_depth, 0, true))));
-    stnt(&a.Lout[i], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-  }
+// Bounce 0 has no stream: the path in slot i (= its stream position) is the
+// camera ray GetRay (camera.go:368-434) of pixel pixels[i % npix], sample
+// sample_base + i / npix, regenerated where it is needed (k_extend and
+// k_shade of the first bounce) instead of written out and read back.
+__device__ __forceinline__ uint32_t slot_pixel(const WaveArgs& a, uint32_t i) {
+  return a.pixels[GIX(i % a.npix, a.npix, 51)];
+}
+__device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a, uint32_t i, uint32_t pix,
+                                           uint32_t sample_base, V3& ro, V3& rd, uint32_t& key) {
+  const int px = int(pix % uint32_t(cam.width)), py = int(pix / uint32_t(cam.width));
+  key = path_key(a.seed, pix, sample_base + i / a.npix);
+  float time;
+  get_ray(cam, px, py, key, ro, rd, time);   // time is recomputed from the key (ray_time) where needed
 }
 
 // ---------------------------------------------------------------- claim pool
@@ -184,10 +180,13 @@ __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_
 // Each lane holds the ray it traverses (p) and a prefetched next ray (pn):
 // the prefetch's loads are in flight while the lane traverses, so a lane
 // that finishes starts its next ray on the following step without waiting.
-template <int STACK, bool kCount, bool kVol>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_extend(DScene sc, WaveArgs a, PathStream cs,
-                                                                const uint32_t* count, uint32_t* zero_a,
-                                                                uint32_t* zero_b, uint32_t* zero_c, uint32_t* fetch) {
+// kFirst: bounce 0, the rays are the camera rays of the claimed slots (the
+// prefetch loads only the slot's pixel; GetRay runs when the ray starts).
+template <int STACK, bool kCount, bool kVol, bool kFirst>
+__global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_extend(DScene sc, DCamera cam, WaveArgs a,
+                                                                PathStream cs, const uint32_t* count,
+                                                                uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
+                                                                uint32_t* fetch, uint32_t sample_base) {
   __shared__ uint32_t lds_stack[(STACK + RTG_WR_WORDS) * 256];   // stack ring + world ray
   // next stream's count, the shadow job count and the shadow fetch counter
   if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
@@ -206,6 +205,13 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       p = pn;
       pn = ITEM_NONE;
       if (kCount) cnt.rays++;
+      if (kFirst) {
+        V3 ro, rd;
+        uint32_t key;
+        camera_ray(cam, a, p, asu(po.x), sample_base, ro, rd, key);
+        po = make_float4(ro.x, ro.y, ro.z, 0.0f);
+        pd = make_float4(rd.x, rd.y, rd.z, asf(key));
+      }
       const int s = trav_init<false, kCount>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), ray_time(asu(pd.w)),
                                              0.001f, __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
@@ -213,9 +219,13 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
     const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
       pn = GIX(idx, a.slots, 40);
-      po = ldnt(&cs.o[pn]);
-      pd = ldnt(&cs.d[pn]);
-      if (kVol) pb = (asu(ldnt(&cs.beta[pn]).w) >> 16) & 0x7FFFu;
+      if (kFirst) {
+        po.x = asf(slot_pixel(a, pn));   // the ray itself is made when it starts
+      } else {
+        po = ldnt(&cs.o[pn]);
+        pd = ldnt(&cs.d[pn]);
+        if (kVol) pb = (asu(ldnt(&cs.beta[pn]).w) >> 16) & 0x7FFFu;
+      }
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (P.dry) break;
@@ -263,9 +273,12 @@ constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 1
 #endif
-template <bool kCount, bool kEnvIS, bool kFancy>
+// kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
+// and this kernel initialises the slot's radiance in Lout.
+template <bool kCount, bool kEnvIS, bool kFancy, bool kFirst>
 __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
-                                               const uint32_t* count, PathStream ns, uint32_t* ncount) {
+                                               const uint32_t* count, PathStream ns, uint32_t* ncount,
+                                               uint32_t sample_base) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
   // sit on every path's dependent-load chain (hit -> material -> texture,
   // light -> light material -> texture).
@@ -298,31 +311,48 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
     float tmax_a = 0.0f;
     V3 P = mk(0.0f, 0.0f, 0.0f), sd = P, beta = P, nbeta = P, ca = P, ch = P, da = P, dh = P;
     // L += beta * e on the path's radiance in Lout[slot] (camera.go:466, :481);
-    // adding an exact zero (black background) leaves L unchanged, so it is skipped
+    // adding an exact zero (black background) leaves L unchanged, so it is
+    // skipped.  At bounce 0 the radiance starts at 0 here (0 + beta * e).
+    bool lout_set = false;
     auto add_L = [&](V3 e) {
       if (e.x == 0.0f && e.y == 0.0f && e.z == 0.0f) return;
       float4* lp = &a.Lout[GIX(slot, a.slots, 44)];
-      const float4 l4 = ldnt(lp);
+      const float4 l4 = kFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ldnt(lp);
       const V3 L = add(mk(l4.x, l4.y, l4.z), mul(beta, e));
       stnt(lp, make_float4(L.x, L.y, L.z, 0.0f));
+      lout_set = true;
     };
     if (live) {
       if (kCount) cnt.rays++;                                    // paths shaded
       const uint32_t ii = GIX(i, a.slots, 41);
-      const float4 h = ldnt(&a.hit[ii]), o4 = ldnt(&cs.o[ii]), d4 = ldnt(&cs.d[ii]), b4 = ldnt(&cs.beta[ii]);
-      key = asu(d4.w);
-      slot = asu(o4.w);
-      const uint32_t st = asu(b4.w);
-      const int dleft = int(st & 0xFFFFu);
-      bounce = (st >> 16) & 0x7FFFu;
-      const bool allow = (st >> 31) != 0u;
-      const V3 ro = mk(o4.x, o4.y, o4.z), rd = mk(d4.x, d4.y, d4.z);
+      const float4 h = ldnt(&a.hit[ii]);
+      V3 ro, rd;
+      int dleft;
+      bool allow;
+      if (kFirst) {
+        slot = ii;
+        camera_ray(cam, a, ii, slot_pixel(a, ii), sample_base, ro, rd, key);
+        dleft = a.max_depth;
+        bounce = 0;
+        allow = true;
+        beta = mk(1.0f, 1.0f, 1.0f);
+      } else {
+        const float4 o4 = ldnt(&cs.o[ii]), d4 = ldnt(&cs.d[ii]), b4 = ldnt(&cs.beta[ii]);
+        key = asu(d4.w);
+        slot = asu(o4.w);
+        const uint32_t st = asu(b4.w);
+        dleft = int(st & 0xFFFFu);
+        bounce = (st >> 16) & 0x7FFFu;
+        allow = (st >> 31) != 0u;
+        ro = mk(o4.x, o4.y, o4.z);
+        rd = mk(d4.x, d4.y, d4.z);
+        beta = mk(b4.x, b4.y, b4.z);
+      }
       const float time = ray_time(key);
-      beta = mk(b4.x, b4.y, b4.z);
       const uint32_t kh = asu(h.y);
 #ifdef RTG_GUARD
       if (kh == 0xFFFFFFFFu && atomicAdd(&rtg_guard_hits, 1) < 16)
-        printf("RTG_GUARD site 50: hit %u of %u never written (bounce %u)\n", i, n, (asu(b4.w) >> 16) & 0x7FFFu);
+        printf("RTG_GUARD site 50: hit %u of %u never written (bounce %u)\n", i, n, bounce);
 #endif
       if (kh == 0u) {                                            // miss (camera.go:451-466)
         V3 bg;
@@ -460,6 +490,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
         }
       }
     }
+    if (kFirst && live && !lout_set) stnt(&a.Lout[GIX(slot, a.slots, 44)], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     uint32_t jc = 0, js = 0;
     block_reserve2(cont, want_shadow, ncount, a.counts + CNT_SHADOW, s_w[par], s_b[par], jc, js);
     if (cont) {
@@ -670,14 +701,11 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
   for (uint32_t s0 = 0; s0 < plan.spp; s0 += plan.samples_per_batch) {
     const uint32_t sb = plan.spp - s0 < plan.samples_per_batch ? plan.spp - s0 : plan.samples_per_batch;
     const uint32_t nslots = sb * a.npix;
+    const uint32_t sample_base = plan.sample_offset + s0;
     hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, a.counts, nslots);
-    hipLaunchKernelGGL(k_camera, dim3(grid_for((const void*)k_camera, 256, 0, nslots, cus)), dim3(256), 0, st, cam, a,
-                       a.s[0], nslots, plan.sample_offset + s0);
     if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
     const int max_trav_blocks = int(a.spill_lanes / 256u);   // one spill column per resident lane
-    int gext = grid_for((const void*)k_extend<STACK, kCount, kVol>, 256, 0, nslots, cus);
-    gext = gext < max_trav_blocks ? gext : max_trav_blocks;
-    const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy>, 256, 0, nslots, cus);
+    const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, 0, nslots, cus);
     int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS>, 256, 0, nslots, cus);
     gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;
     const int gap = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
@@ -688,11 +716,26 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
       if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
 #endif
       if ((e = mark(plan, KC_EXTEND, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_extend<STACK, kCount, kVol>), dim3(gext), dim3(256), 0, st, sc, a, a.s[c], cnt_stream[c],
-                         cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext);
-      if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
-                         cnt_stream[c], a.s[nx], cnt_stream[nx]);
+      // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
+      if (b == 0) {
+        const void* fx = (const void*)k_extend<STACK, kCount, kVol, true>;
+        int gext = grid_for(fx, 256, 0, nslots, cus);
+        gext = gext < max_trav_blocks ? gext : max_trav_blocks;
+        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
+                           cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+        if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
+                           cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+      } else {
+        const void* fx = (const void*)k_extend<STACK, kCount, kVol, false>;
+        int gext = grid_for(fx, 256, 0, nslots, cus);
+        gext = gext < max_trav_blocks ? gext : max_trav_blocks;
+        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
+                           cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+        if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
+                           cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+      }
       if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS>), dim3(gsd), dim3(256), 0, st, sc, a, cnt_shadow,
                          fetch_sh, fetch_ext);

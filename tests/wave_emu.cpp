@@ -35,11 +35,17 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
     const uint32_t sb = spp - s0 < spb ? spp - s0 : spb;
     const uint32_t nslots = sb * a.npix;
     k_set_counts(a.counts, nslots);
-    k_camera(cam, a, a.s[0], nslots, s0);
     for (int b = 0; b < max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
-      k_extend<kRing, false, kVol>(sc, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext);
-      k_shade<false, kEnvIS, kFancy>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx]);
+      if (b == 0) {
+        k_extend<kRing, false, kVol, true>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
+                                           fetch_ext, s0);
+        k_shade<false, kEnvIS, kFancy, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
+      } else {
+        k_extend<kRing, false, kVol, false>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
+                                            fetch_ext, s0);
+        k_shade<false, kEnvIS, kFancy, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
+      }
       k_shadow<kRing, false, kVol, kEnvIS>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
       k_nee_apply<kEnvIS>(a, cnt_shadow);
     }

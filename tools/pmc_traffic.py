@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def family(name):
-    for k in ("k_extend", "k_shade", "k_shadow", "k_camera", "k_accum", "k_finalize"):
+    for k in ("k_extend", "k_shade", "k_shadow", "k_nee_apply", "k_accum", "k_finalize"):
         if f"rtg::{k}<" in name or f"rtg::{k}(" in name:
             return k[2:]
     return None
