@@ -1,0 +1,175 @@
+// gpu_bucket_renderer.go — NewGPUBucketRenderer: BucketRenderer's three
+// progressive passes (bucket_renderer.go:127-213) with each pass rendered by
+// librtgpu.so on an MI355X instead of numWorkers goroutines.
+//
+// COMPILE-UNVERIFIED: no Go toolchain in this repository's build image.  Copy
+// to rt/ of byvfx/go-raytracing next to gpu_flatten.go; main.go:86 then reads
+//
+//	renderer := rt.NewGPUBucketRenderer(camera, bvh, bucketSize, numWorkers)
+//
+// and ebiten.RunGame(renderer) is unchanged.  The type embeds the CPU
+// renderer, so Draw / Layout / SaveImage / IsCompleted / GetRenderDuration
+// and the stats overlay are the reference's own code; only Update differs.
+// The same schedule is implemented in C++ by librtscene.so (rts_renderer_*),
+// which tests/test_gpu_parity.py::test_bucket_renderer_three_passes checks
+// against the CPU oracle.
+package rt
+
+import (
+	"fmt"
+	"os"
+	"time"
+
+	"go-raytracing/rtgpu"
+)
+
+// gpuChunkBuckets is how many buckets one rt_render call takes: a chunk of
+// 64 32x32 buckets is ~65K pixels (enough to fill the GPU at 1 spp) and
+// keeps the window's progress bar moving during a long pass.
+const gpuChunkBuckets = 64
+
+// GPUBucketRenderer is a BucketRenderer whose passes run on the GPU.  When
+// the scene holds something the GPU path does not take (rtgpu.IsUnsupported)
+// or no device is present, gpu is nil and every method is the CPU
+// renderer's.
+type GPUBucketRenderer struct {
+	*BucketRenderer
+	gpu     *rtgpu.Ctx
+	cam     rtgpu.CameraDesc
+	buckets []rtgpu.Bucket // r.buckets (centre-out order of generateBuckets)
+	accum   []float32      // per-pixel radiance sums of the pass in flight
+	rgba    []byte         // tonemapped frame of the pass in flight
+	seed    uint32
+	err     error // first GPU error; the render stops there
+}
+
+// NewGPUBucketRenderer has NewBucketRenderer's signature
+// (bucket_renderer.go:54-74); numWorkers only matters for the CPU fallback.
+func NewGPUBucketRenderer(camera *Camera, world Hittable, bucketSize int, numWorkers int) *GPUBucketRenderer {
+	g := &GPUBucketRenderer{BucketRenderer: NewBucketRenderer(camera, world, bucketSize, numWorkers), seed: 1}
+	if err := g.initGPU(camera, world); err != nil {
+		fmt.Fprintf(os.Stderr, "GPU renderer unavailable (%v); rendering on the CPU\n", err)
+		if g.gpu != nil {
+			g.gpu.Close()
+			g.gpu = nil
+		}
+	}
+	return g
+}
+
+func (g *GPUBucketRenderer) initGPU(camera *Camera, world Hittable) error {
+	camera.Initialize() // the state GetRay reads (camera.go:286-344); idempotent
+	scene, err := FlattenForGPU(world, camera)
+	if err != nil {
+		return err
+	}
+	if g.gpu, err = rtgpu.New(0); err != nil {
+		return err
+	}
+	if err = g.gpu.Upload(scene); err != nil {
+		return err
+	}
+	g.cam = GPUCameraDesc(camera)
+	g.buckets = make([]rtgpu.Bucket, len(g.BucketRenderer.buckets))
+	for i, b := range g.BucketRenderer.buckets {
+		g.buckets[i] = rtgpu.Bucket{X: int32(b.X), Y: int32(b.Y), Width: int32(b.Width), Height: int32(b.Height)}
+	}
+	n := camera.ImageWidth * camera.ImageHeight
+	g.accum = make([]float32, 3*n)
+	g.rgba = make([]byte, 4*n)
+	return nil
+}
+
+// Close releases the device context (the CPU renderer has nothing to free).
+func (g *GPUBucketRenderer) Close() {
+	if g.gpu != nil {
+		g.gpu.Close()
+		g.gpu = nil
+	}
+}
+
+// Update is BucketRenderer.Update (bucket_renderer.go:127-165) with the pass
+// body swapped for gpuPass.
+func (g *GPUBucketRenderer) Update() error {
+	if g.gpu == nil {
+		return g.BucketRenderer.Update()
+	}
+	r := g.BucketRenderer
+	if r.completed {
+		return nil
+	}
+	r.mu.Lock()
+	if !r.renderStarted {
+		r.renderStarted = true
+		r.mu.Unlock()
+		go g.gpuPass()
+	} else {
+		r.mu.Unlock()
+	}
+	if r.passComplete.Load() && r.currentPass < r.totalPasses {
+		r.passComplete.Store(false)
+		r.completedCount.Store(0)
+		r.currentPass++
+		if r.currentPass < r.totalPasses && g.err == nil {
+			go g.gpuPass()
+		} else {
+			r.completed = true
+			r.renderEnd = time.Now()
+			if g.err != nil {
+				fmt.Fprintf(os.Stderr, "GPU render failed: %v\n", g.err)
+			}
+			r.drawStatsToFramebuffer()
+			_ = r.SaveImage("image.png")
+			PrintRenderStats(r.renderEnd.Sub(r.renderStart), r.camera.ImageWidth, r.camera.ImageHeight)
+			g.Close()
+		}
+	}
+	return nil
+}
+
+// passQuality is renderPass's schedule (bucket_renderer.go:175-191).
+func passQuality(pass int, c *Camera) (spp, depth int) {
+	switch pass {
+	case 0:
+		return 1, 3
+	case 1:
+		return max(1, c.SamplesPerPixel/4), max(3, c.MaxDepth/2)
+	default:
+		return c.SamplesPerPixel, c.MaxDepth
+	}
+}
+
+// gpuPass renders the current pass chunk by chunk in bucket order; each
+// chunk overwrites its buckets' sums (renderBucketWithQuality writes every
+// bucket pixel each pass), is tonemapped on the device with
+// bucket_renderer.go:276-285's quantisation and copied into the
+// framebuffer bucket by bucket under r.mu, as renderBucketWithQuality does.
+func (g *GPUBucketRenderer) gpuPass() {
+	r := g.BucketRenderer
+	spp, depth := passQuality(r.currentPass, r.camera)
+	w, h := r.camera.ImageWidth, r.camera.ImageHeight
+	seed := g.seed + uint32(r.currentPass)*0x9E3779B9 // one RNG stream per pass
+	for lo := 0; lo < len(g.buckets) && g.err == nil; lo += gpuChunkBuckets {
+		hi := min(lo+gpuChunkBuckets, len(g.buckets))
+		chunk := g.buckets[lo:hi]
+		_, err := g.gpu.Render(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
+			Buckets: chunk}, g.accum)
+		if err == nil {
+			err = g.gpu.Tonemap(g.accum, w, h, spp, g.rgba)
+		}
+		if err != nil {
+			g.err = err
+			break
+		}
+		r.mu.Lock()
+		for _, b := range chunk {
+			for y := int(b.Y); y < int(b.Y+b.Height); y++ {
+				row := (y*w + int(b.X)) * 4
+				copy(r.framebuffer.Pix[row:row+int(b.Width)*4], g.rgba[row:row+int(b.Width)*4])
+			}
+		}
+		r.mu.Unlock()
+		r.completedCount.Add(int32(len(chunk)))
+	}
+	r.passComplete.Store(true)
+}
