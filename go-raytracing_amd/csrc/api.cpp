@@ -98,18 +98,21 @@ int ensure(rt_ctx* ctx, DevBuf& b, size_t bytes) {
   return RT_OK;
 }
 
-// Copies `v` to a new device buffer with room for `extra` more elements.
+// Copies `v` to a new device buffer with room for `extra` more elements and
+// kSceneSlack bytes past them: the traversal reads a record as whole 16-B
+// vectors from its 4-B-aligned start (the phase-2 gather, device_common.h),
+// which may run up to 112 B past the record.
+constexpr size_t kSceneSlack = 128;
 template <typename T>
 int upload_vec(rt_ctx* ctx, const std::vector<T>& v, const T** dst, size_t extra = 0) {
   DevBuf b;
-  size_t bytes = std::max<size_t>((v.size() + extra) * sizeof(T), 16);
+  size_t bytes = (v.size() + extra) * sizeof(T) + kSceneSlack;
   hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scene)");
   b.bytes = bytes;
-  if (!v.empty()) {
-    e = hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
-    if (e != hipSuccess) { (void)hipFree(b.p); return hip_fail(ctx, e, "hipMemcpy(scene)"); }
-  }
+  e = hipMemset(b.p, 0, bytes);
+  if (e == hipSuccess && !v.empty()) e = hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(b.p); return hip_fail(ctx, e, "hipMemcpy(scene)"); }
   ctx->scene_bufs.push_back(b);
   ctx->scene_bytes += bytes;
   *dst = static_cast<const T*>(b.p);
@@ -337,7 +340,13 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // LDS stack ring (8 entries per lane by default, 16 with RTGPU_STACK=16) +
   // global spill
   // up to kStackMax: scenes of any supported depth run with the small ring.
-  static const int lds_stack = [] { const char* e = getenv("RTGPU_STACK"); return e && atoi(e) == 16 ? 16 : 8; }();
+  static const int lds_stack = [] {
+    const char* e = getenv("RTGPU_STACK");
+#ifdef RTG_RING24
+    if (e && atoi(e) == 24) return 24;   // diagnostic build only
+#endif
+    return e && atoi(e) == 16 ? 16 : 8;
+  }();
   const int stack = lds_stack;
   a.spill_lanes = uint32_t(std::max(1, ctx->num_cus)) * kSpillLanesPerCU;
   a.spill_cap = kStackMax - stack;

@@ -175,9 +175,9 @@ struct alignas(128) DInstEntry {
   float chi[3]; int32_t nwrap;       // culling box hi
   float p0[3]; uint32_t root_item;   // wrapper 0 ray-side floats: translate: offset; rotate: sin, cos, -;
   float p1[3]; int32_t check_box;    //   scale: 1/factor;  BLAS root item, root-box test flag
-  float p2[3]; int32_t pad0;
   float rlo[3]; int32_t pad1;        // BLAS root box (object space)
   float rhi[3]; int32_t pad2;
+  float p2[3]; int32_t pad0;         // (the traversal gathers the first 112 B: wrappers 0-2 + root box)
   float p3[3]; int32_t pad3;
   float p4[3]; int32_t pad4;         // second line: wrappers 4 and 5 (rare)
   float p5[3]; int32_t pad5;

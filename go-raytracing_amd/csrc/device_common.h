@@ -473,13 +473,11 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
 // ----------------------------------------------------------------------------
 constexpr uint32_t ITEM_NONE = 0xFFFFFFFFu;
-// RTG_WIDE_CLOSEST: the closest-hit traversal also issues its leaf and
-// instance-record loads together (as the any-hit one does) — it needs the
-// registers of a lower occupancy (tuning knob).
-#ifdef RTG_WIDE_CLOSEST
-constexpr bool kWideClosest = true;
+// 16-B vector at 4-B alignment (one dwordx4 load from a packed record)
+#ifdef RTG_HOST_EMU
+struct rtg_f4u { float x, y, z, w; };
 #else
-constexpr bool kWideClosest = false;
+typedef float rtg_f4u __attribute__((ext_vector_type(4), aligned(4)));
 #endif
 constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the stack"
 
@@ -529,13 +527,19 @@ struct TStack {
     return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]);
   }
 #endif
+#ifdef RTG_RING24
+  // diagnostic build only: a 24-entry ring is not a power of two
+  __device__ __forceinline__ int ring(int sp) const { return int(uint32_t(sp) % uint32_t(cap)); }
+#else
+  __device__ __forceinline__ int ring(int sp) const { return sp & (cap - 1); }
+#endif
   __device__ __forceinline__ void push(int sp, uint32_t v) const {
-    uint32_t* slot = lds + (sp & (cap - 1)) * stride;
+    uint32_t* slot = lds + ring(sp) * stride;
     if (sp >= cap) *spill_at(sp - cap) = *slot;
     *slot = v;
   }
   __device__ __forceinline__ uint32_t pop(int sp) const {   // sp = new depth
-    uint32_t* slot = lds + (sp & (cap - 1)) * stride;
+    uint32_t* slot = lds + ring(sp) * stride;
     const uint32_t v = *slot;
     if (sp >= cap) *slot = *spill_at(sp - cap);
     return v;
@@ -715,47 +719,50 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const uint32_t sa = rtg_stamp();
 #endif
     const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
+    const bool is_inst = tag == ITEM_INSTANCE || tag == ITEM_WINST;
+    // One gather per round for the record the postponed item names (the
+    // first two triangles of a triangle leaf, a world quad / sphere, a leaf
+    // header, an instance entry): every lane's loads are issued together, so
+    // a wave whose lanes hold different kinds of items waits for memory once
+    // per round instead of once per kind.  Records are read as 80 B (112 B for
+    // an instance entry) at their 4-B-aligned start; every scene array has
+    // 128 B of slack at its end (upload_vec).
+    const char* rec = reinterpret_cast<const char*>(sc.nodes);   // INST_END: no record, any readable line
+    if (item_is_tri_leaf(tag)) rec = reinterpret_cast<const char*>(sc.tris + GIX(idx, sc.n_tris, 12));
+    else if (tag == ITEM_LEAF) rec = reinterpret_cast<const char*>(sc.leaves + GIX(idx, sc.n_leaves, 10));
+    else if (tag == ITEM_WQUAD) rec = reinterpret_cast<const char*>(sc.quads + GIX(idx, sc.n_quads, 37));
+    else if (tag == ITEM_WSPHERE) rec = reinterpret_cast<const char*>(sc.spheres + GIX(idx, sc.n_spheres, 38));
+    else if (is_inst) rec = reinterpret_cast<const char*>(sc.inst_entry + GIX(idx, sc.n_refs, 17));
+    const rtg_f4u* const g = reinterpret_cast<const rtg_f4u*>(rec);
+    const rtg_f4u g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4];
+    rtg_f4u g5 = {0.0f, 0.0f, 0.0f, 0.0f}, g6 = g5;
+    if (is_inst) { g5 = g[5]; g6 = g[6]; }
     if (item_is_tri_leaf(tag)) {
-      // inline triangle leaf (BLAS, tested once; the host SAH builder's
-      // leaves hold <= 2): any-hit rays take the triangles two at a time, both
-      // loads issued before either test (the second index repeats the first
-      // when there is none); measured the faster form in each kernel
+      // inline triangle leaf (BLAS, tested once): the first two triangles
+      // come from the gather, any further ones (reference-topology leaves)
+      // are loaded one at a time
       const int n = int(tag - ITEM_TRI1) + 1;
       const bool world = T.cur_ref < 0;
-      if constexpr (kAny || kWideClosest) {   // both loads of a pair issued before either test
-        for (int k = 0; k < n; k += 2) {
-          const uint32_t pa = idx + uint32_t(k), pb = k + 1 < n ? pa + 1u : pa;
-          const DTri ta = sc.tris[GIX(pa, sc.n_tris, 12)], tb = sc.tris[GIX(pb, sc.n_tris, 12)];
-          for (int j = 0; j < 2 && k + j < n; ++j) {
-            float t = 0.0f;
-            if (kCount) cnt.tri++;
-            if (!tri_t(j ? tb : ta, T.cr.o, T.cr.d, T.tmin, t)) continue;
-            if (kAny) { if (t <= T.tmax) return TRAV_ANYHIT; continue; }
-            const int pos = int(pa) + j;
-            const int refpos = world ? pos : T.cur_ref;
-            const int primpos = world ? 0 : (PRIM_IN_INST | pos);
-            if (accept(sc, t, PK_TRI, refpos, primpos, best)) {
-              best.t = t; best.kind = PK_TRI; best.idx = pos;
-              best.refpos = refpos; best.primpos = primpos;
-            }
-          }
+      bool any = false;
+      auto tri_one = [&](const DTri& tr, int pos) {
+        float t = 0.0f;
+        if (kCount) cnt.tri++;
+        if (!tri_t(tr, T.cr.o, T.cr.d, T.tmin, t)) return;
+        if (kAny) { any = any || t <= T.tmax; return; }
+        const int refpos = world ? pos : T.cur_ref;
+        const int primpos = world ? 0 : (PRIM_IN_INST | pos);
+        if (accept(sc, t, PK_TRI, refpos, primpos, best)) {
+          best.t = t; best.kind = PK_TRI; best.idx = pos;
+          best.refpos = refpos; best.primpos = primpos;
         }
-      } else {   // closest hit: one triangle at a time (a pair spills registers here)
-        for (int k = 0; k < n; ++k) {
-          const int pos = int(idx) + k;
-          float t = 0.0f;
-          if (kCount) cnt.tri++;
-          if (!tri_t(sc.tris[GIX(pos, sc.n_tris, 12)], T.cr.o, T.cr.d, T.tmin, t)) continue;
-          const int refpos = world ? pos : T.cur_ref;
-          const int primpos = world ? 0 : (PRIM_IN_INST | pos);
-          if (accept(sc, t, PK_TRI, refpos, primpos, best)) {
-            best.t = t; best.kind = PK_TRI; best.idx = pos;
-            best.refpos = refpos; best.primpos = primpos;
-          }
-        }
-      }
+      };
+      tri_one(DTri{{g0.x, g0.y, g0.z}, {g0.w, g1.x, g1.y}, {g1.z, g1.w, g2.x}}, int(idx));
+      if (kAny && any) return TRAV_ANYHIT;
+      if (n > 1) tri_one(DTri{{g2.y, g2.z, g2.w}, {g3.x, g3.y, g3.z}, {g3.w, g4.x, g4.y}}, int(idx) + 1);
+      for (int k = 2; k < n; ++k) tri_one(sc.tris[GIX(idx + uint32_t(k), sc.n_tris, 12)], int(idx) + k);
+      if (kAny && any) return TRAV_ANYHIT;
     } else if (tag == ITEM_LEAF) {
-      const DLeaf leaf = sc.leaves[GIX(idx, sc.n_leaves, 10)];
+      const DLeaf leaf{__float_as_uint(g0.x), __float_as_uint(g0.y)};
       const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
       const bool world = T.cur_ref < 0;
       for (int k = 0; k < n; ++k) {
@@ -808,11 +815,20 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       if (tag == ITEM_WQUAD) {
         pk = PK_QUAD;
         if (kCount) cnt.quad++;
-        ok = quad_t(sc.quads[GIX(idx, sc.n_quads, 37)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
+        DQuad q;
+        q.Qx = g0.x; q.Qy = g0.y; q.Qz = g0.z; q.D = g0.w;
+        q.nx = g1.x; q.ny = g1.y; q.nz = g1.z; q.mat = 0;
+        q.ux = g2.x; q.uy = g2.y; q.uz = g2.z; q.pad0 = 0.0f;
+        q.vx = g3.x; q.vy = g3.y; q.vz = g3.z; q.pad1 = 0.0f;
+        q.wx = g4.x; q.wy = g4.y; q.wz = g4.z; q.pad2 = 0.0f;
+        ok = quad_t(q, T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
       } else {
         pk = PK_SPHERE;
         if (kCount) cnt.sph++;
-        ok = sphere_t(sc.spheres[GIX(idx, sc.n_spheres, 38)], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+        DSphere sp;
+        sp.cx = g0.x; sp.cy = g0.y; sp.cz = g0.z; sp.r = g0.w;
+        sp.vx = g1.x; sp.vy = g1.y; sp.vz = g1.z; sp.mat = 0;
+        ok = sphere_t(sp, T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
       }
       if (ok) {
         if (kAny) return TRAV_ANYHIT;
@@ -822,84 +838,46 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           best.refpos = refpos; best.primpos = 0;
         }
       }
-    } else if (tag == ITEM_INSTANCE || tag == ITEM_WINST) {
-      // One entry record per instance ref (DInstEntry): for a world leaf of
-      // one instance (ITEM_WINST) first the world-space cull on the
-      // instance's own padded bbox (an ITEM_INSTANCE from a leaf of several
-      // objects was culled there), then the wrapper chain (the ray into
-      // object space, transform.go) and the BLAS root: one line instead of
-      // the dependent leaf -> refs -> culling box -> DInstance -> DBvh loads.
-      // The any-hit kernel loads the line as five float4s issued together;
-      // the closest-hit kernel, whose registers are tighter (the hit
-      // record), field by field (each form measured the faster in its kernel).
+    } else if (is_inst) {
+      // One entry record per instance ref (DInstEntry, from the gather): for
+      // a world leaf of one instance (ITEM_WINST) first the world-space cull
+      // on the instance's own padded bbox (an ITEM_INSTANCE from a leaf of
+      // several objects was culled there), then the wrapper chain (the ray
+      // into object space, transform.go) and the BLAS root box.
       const bool winst = tag == ITEM_WINST;
       const float hi = kAny ? T.tmax : best.t;
       float tn = 0.0f;
-      if constexpr (!kAny && !kWideClosest) {
-        const DInstEntry& E = sc.inst_entry[GIX(idx, sc.n_refs, 17)];
-        bool go = true;
-        if (winst) {
-          if (kCount) cnt.ibox++;
-          go = box_hit(E.clo[0], E.chi[0], E.clo[1], E.chi[1], E.clo[2], E.chi[2], T.cr, T.tmin, hi, tn);
+      bool go = true;
+      if (winst) {
+        if (kCount) cnt.ibox++;
+        go = box_hit(g0.x, g1.x, g0.y, g1.y, g0.z, g1.z, T.cr, T.tmin, hi, tn);
+      }
+      if (go) {
+        if (kCount) cnt.inst++;
+        const uint32_t kinds = __float_as_uint(g0.w);
+        const int nwrap = int(__float_as_uint(g1.w));
+        V3 o = S.wo(), d = S.wd();
+        auto wr = [&](int i, float a, float b, float c) {
+          if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), a, b, c, o, d);
+        };
+        wr(0, g2.x, g2.y, g2.z);
+        wr(1, g3.x, g3.y, g3.z);
+        wr(2, g6.x, g6.y, g6.z);
+        if (nwrap > 3) {
+          const DInstEntry& E = sc.inst_entry[GIX(idx, sc.n_refs, 17)];
+          wr(3, E.p3[0], E.p3[1], E.p3[2]);
+          wr(4, E.p4[0], E.p4[1], E.p4[2]);
+          wr(5, E.p5[0], E.p5[1], E.p5[2]);
         }
-        if (go) {
-          if (kCount) cnt.inst++;
-          V3 o = S.wo(), d = S.wd();
-          const uint32_t kinds = E.kinds;
-          const int nwrap = E.nwrap;
-          auto wr = [&](int i, const float* q) {
-            if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), q[0], q[1], q[2], o, d);
-          };
-          wr(0, E.p0); wr(1, E.p1); wr(2, E.p2);
-          if (nwrap > 3) { wr(3, E.p3); wr(4, E.p4); wr(5, E.p5); }
-          const TRay orr = make_tray(o, d);
-          bool enter = true;
-          if (E.check_box)   // BVHNode.Hit tests its own bbox first
-            enter = box_hit(E.rlo[0], E.rhi[0], E.rlo[1], E.rhi[1], E.rlo[2], E.rhi[2], orr, T.tmin, hi, tn);
-          if (enter) {
-            if (T.item < ITEM_POP) push(T.item);
-            push(ITEM_INST_END << ITEM_SHIFT);
-            T.cr = orr; T.cur_ref = int(idx);
-            T.item = E.root_item;
-          }
-        }
-      } else {
-        const float4* e4 = reinterpret_cast<const float4*>(sc.inst_entry + GIX(idx, sc.n_refs, 17));
-        const float4 c0 = e4[0], c1 = e4[1], q0 = e4[2], q1 = e4[3], q2 = e4[4];
-        bool go = true;
-        if (winst) {
-          if (kCount) cnt.ibox++;
-          go = box_hit(c0.x, c1.x, c0.y, c1.y, c0.z, c1.z, T.cr, T.tmin, hi, tn);
-        }
-        if (go) {
-          if (kCount) cnt.inst++;
-          const uint32_t kinds = __float_as_uint(c0.w);
-          const int nwrap = int(__float_as_uint(c1.w));
-          V3 o = S.wo(), d = S.wd();
-          auto wr = [&](int i, float a, float b, float c) {
-            if (i < nwrap) wrap_ray3(int((kinds >> (4 * i)) & 15u), a, b, c, o, d);
-          };
-          wr(0, q0.x, q0.y, q0.z);
-          wr(1, q1.x, q1.y, q1.z);
-          wr(2, q2.x, q2.y, q2.z);
-          if (nwrap > 3) {
-            const float4 q3 = e4[7], q4 = e4[8], q5 = e4[9];
-            wr(3, q3.x, q3.y, q3.z);
-            wr(4, q4.x, q4.y, q4.z);
-            wr(5, q5.x, q5.y, q5.z);
-          }
-          const TRay orr = make_tray(o, d);
-          bool enter = true;
-          if (__float_as_uint(q1.w) != 0u) {   // check_box: BVHNode.Hit tests its own bbox first
-            const float4 r0 = e4[5], r1 = e4[6];
-            enter = box_hit(r0.x, r1.x, r0.y, r1.y, r0.z, r1.z, orr, T.tmin, hi, tn);
-          }
-          if (enter) {
-            if (T.item < ITEM_POP) push(T.item);
-            push(ITEM_INST_END << ITEM_SHIFT);
-            T.cr = orr; T.cur_ref = int(idx);
-            T.item = __float_as_uint(q0.w);   // BLAS root item
-          }
+        const TRay orr = make_tray(o, d);
+        bool enter = true;
+        if (__float_as_uint(g3.w) != 0u)   // check_box: BVHNode.Hit tests its own bbox first
+          enter = box_hit(g4.x, g5.x, g4.y, g5.y, g4.z, g5.z, orr, T.tmin, hi, tn);
+        if (enter) {
+          if (T.item < ITEM_POP) push(T.item);
+          push(ITEM_INST_END << ITEM_SHIFT);
+          T.cr = orr; T.cur_ref = int(idx);
+          T.item = __float_as_uint(g2.w);   // BLAS root item
         }
       }
     } else {  // ITEM_INST_END: back to the world-space ray
@@ -912,6 +890,11 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     // ITEM_NONE here only means the stack was empty when this lane last
     // popped; the leaf just processed may have pushed instance items since.
     if (T.item == ITEM_POP || T.item == ITEM_NONE) T.item = pop();
+    // leaving an instance: restore the world ray here, not in another round
+    while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END) {
+      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
+      T.item = pop();
+    }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE) postpone();
 #ifdef RTG_STAMP
     if (st_l) {

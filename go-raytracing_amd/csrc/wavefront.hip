@@ -776,6 +776,13 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     }                                                                             \
   } while (0)
     const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0;
+#ifdef RTG_RING24
+    // diagnostic build only: the 24-entry ring of the round-1 fault
+    if (stack > 16) {
+      if (vol) { if (count) RUN(24, true, true); else RUN(24, false, true); }
+      else { if (count) RUN(24, true, false); else RUN(24, false, false); }
+    } else
+#endif
     if (stack > 8) {
       if (vol) { if (count) RUN(16, true, true); else RUN(16, false, true); }
       else { if (count) RUN(16, true, false); else RUN(16, false, false); }

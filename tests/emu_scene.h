@@ -4,6 +4,8 @@
 #pragma once
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -20,6 +22,9 @@ static const T* ptr(const std::vector<T>& v) { return v.empty() ? nullptr : v.da
 
 struct EmuScene {
   rts_scene* scn = nullptr;
+  // copies of the arrays the traversal gathers from, with the 128 B of slack
+  // the device buffers have (api.cpp upload_vec)
+  std::vector<std::vector<char>> padded;
   HostScene h;
   DScene d{};
   DCamera cam{};
@@ -40,12 +45,21 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   if (flatten_scene(rts_scene_get_desc(E.scn), E.h, ferr)) { fprintf(stderr, "%s\n", ferr.c_str()); return 4; }
   const HostScene& h = E.h;
   DScene& d = E.d;
+  auto pad = [&](const auto& v) {
+    using T = typename std::decay_t<decltype(v)>::value_type;
+    std::vector<char> b(v.size() * sizeof(T) + 128, 0);
+    if (!v.empty()) std::memcpy(b.data(), v.data(), v.size() * sizeof(T));
+    E.padded.push_back(std::move(b));
+    return reinterpret_cast<const T*>(E.padded.back().data());
+  };
+  E.padded.reserve(8);
   d.nodes = ptr(h.nodes4); d.leaves = ptr(h.leaves); d.refs = ptr(h.refs); d.ref_rank = ptr(h.ref_rank);
   d.ref_box = ptr(h.ref_box); d.spheres = ptr(h.spheres); d.quads = ptr(h.quads); d.tris = ptr(h.tris);
   d.tri_aux = ptr(h.tri_aux); d.circles = ptr(h.circles); d.circle_rank = ptr(h.circle_rank);
   d.circle_hidx = ptr(h.circle_hidx); d.perlins = ptr(h.perlins); d.images = ptr(h.images);
   d.image_texels = ptr(h.image_texels); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
   d.inst_entry = ptr(h.inst_entries);
+  d.leaves = pad(h.leaves); d.tris = pad(h.tris); d.quads = pad(h.quads); d.spheres = pad(h.spheres);
   d.quad_wref = ptr(h.quad_wref); d.sphere_wref = ptr(h.sphere_wref);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
   d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
