@@ -533,15 +533,23 @@ struct TStack {
 #else
   __device__ __forceinline__ int ring(int sp) const { return sp & (cap - 1); }
 #endif
-  __device__ __forceinline__ void push(int sp, uint32_t v) const {
+  // The depth bound (cap + spill_cap) is checked only on the spill path: the
+  // common push / pop is one LDS access and one compare against the
+  // compile-time ring size.  Past the bound (an internal error: the host
+  // sizes spill_cap from the scene's stack need) the entry is dropped and
+  // `err` flagged; the spill area is never touched out of range.
+  __device__ __forceinline__ void push(int sp, uint32_t v, int* err) const {
     uint32_t* slot = lds + ring(sp) * stride;
-    if (sp >= cap) *spill_at(sp - cap) = *slot;
+    if (sp >= cap) {
+      if (sp - cap < spill_cap) *spill_at(sp - cap) = *slot;
+      else *err = 1;
+    }
     *slot = v;
   }
   __device__ __forceinline__ uint32_t pop(int sp) const {   // sp = new depth
     uint32_t* slot = lds + ring(sp) * stride;
     const uint32_t v = *slot;
-    if (sp >= cap) *slot = *spill_at(sp - cap);
+    if (sp >= cap && sp - cap < spill_cap) *slot = *spill_at(sp - cap);
     return v;
   }
 };
@@ -622,8 +630,8 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   // and no early exit in the push sequence.
   auto push = [&](uint32_t v) {
     if (kCount && T.sp >= S.cap) cnt.spill++;
-    if (T.sp < S.cap + S.spill_cap) { S.push(T.sp, v); ++T.sp; }
-    else *err = 1;
+    S.push(T.sp, v, err);
+    ++T.sp;
   };
   auto postpone = [&]() {
     T.lf = T.item;
