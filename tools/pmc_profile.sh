@@ -4,7 +4,7 @@
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-count}
+ARGS=${ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-count --no-configs --no-balance}
 mkdir -p $OUT
 run() {
   name=$1; shift
