@@ -377,11 +377,6 @@ __device__ __forceinline__ bool tie_wins(const DScene& sc, int kind, int refpos,
   }
   return cc ? later : !later;
 }
-__device__ __forceinline__ bool accept(const DScene& sc, float t, int kind, int refpos, int primpos, const Best& b) {
-  if (t < b.t) return true;
-  if (t == b.t && b.kind != 0) return tie_wins(sc, kind, refpos, primpos, b.kind, b.refpos, b.primpos);
-  return false;
-}
 
 // Work counters for the instrumented variant (rt_count_work).
 struct Cnt {
@@ -489,9 +484,15 @@ constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the sta
 // The lane's world-space ray (origin, direction, 1/direction) lives beside it
 // in LDS: it is read only on instance entry / exit and volume tests, so it
 // need not occupy nine VGPRs for the whole traversal.
+// The closest-hit record's identity (kind, index, ref / prim positions) sits
+// there too: it is written when a hit is accepted and read only on exact-t
+// ties and when the ray ends, so only the hit distance stays in a register.
 // Only `lds` is per lane (one VGPR); the rest is block-uniform: the lane's
 // spill column is spill_blk + (its LDS slot - lds0), formed on the rare
-// spill path, and the world ray sits at lds + cap * stride.
+// spill path, the world ray sits at lds + cap * stride and the hit record
+// after it.
+constexpr int kWorldRayWords = 9;   // LDS words per lane: world ray
+constexpr int kHitWords = 4;        // LDS words per lane: hit record (closest-hit kernels)
 struct TStack {
   uint32_t* lds;       // this lane's slot 0
   int stride;          // LDS words between slots (lanes interleaved)
@@ -504,13 +505,6 @@ struct TStack {
   __device__ __forceinline__ uint32_t* spill_at(int k) const {
     return spill_blk + (lds - lds0) + size_t(GIX(k, spill_cap, 25)) * sstride;
   }
-#ifdef RTG_WORLD_RAY_REGS
-  mutable V3 wo_, wd_, winv_;
-  __device__ __forceinline__ void save_world(V3 o, V3 d, V3 inv) const { wo_ = o; wd_ = d; winv_ = inv; }
-  __device__ __forceinline__ V3 wo() const { return wo_; }
-  __device__ __forceinline__ V3 wd() const { return wd_; }
-  __device__ __forceinline__ V3 winv() const { return winv_; }
-#else
   __device__ __forceinline__ void save_world(V3 o, V3 d, V3 inv) const {
     float* wr = wrp();
     wr[0] = o.x; wr[stride] = o.y; wr[2 * stride] = o.z;
@@ -526,7 +520,15 @@ struct TStack {
     const float* wr = wrp();
     return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]);
   }
-#endif
+  __device__ __forceinline__ int* hitp() const { return reinterpret_cast<int*>(lds + (cap + kWorldRayWords) * stride); }
+  __device__ __forceinline__ void set_hit(int kind, int idx, int refpos, int primpos) const {
+    int* h = hitp();
+    h[0] = kind; h[stride] = idx; h[2 * stride] = refpos; h[3 * stride] = primpos;
+  }
+  __device__ __forceinline__ int hit_kind() const { return hitp()[0]; }
+  __device__ __forceinline__ int hit_idx() const { return hitp()[stride]; }
+  __device__ __forceinline__ int hit_refpos() const { return hitp()[2 * stride]; }
+  __device__ __forceinline__ int hit_primpos() const { return hitp()[3 * stride]; }
 #ifdef RTG_RING24
   // diagnostic build only: a 24-entry ring is not a power of two
   __device__ __forceinline__ int ring(int sp) const { return int(uint32_t(sp) % uint32_t(cap)); }
@@ -553,7 +555,8 @@ struct TStack {
     return v;
   }
 };
-// LDS words per lane: `cap` stack entries + the 9-float world ray.
+// LDS words per lane: `cap` stack entries + the 9-float world ray (+ the
+// 4-word hit record for closest-hit traversal).
 __device__ __forceinline__ TStack lds_stack_only(uint32_t* lds, int stride, int cap) {
   return TStack{lds, stride, cap, nullptr, lds, 0, 0};
 }
@@ -566,7 +569,8 @@ struct Trav {
   uint32_t key, bounce, voldom;
   uint32_t item, lf;
   int sp, cur_ref;       // cur_ref: TLAS ref of the instance being traversed, -1 in world space
-  Best best;             // best.inst is resolved once at the end (resolve_inst)
+  float bt;              // closest accepted hit distance (tmax: none); the rest of the
+                         // hit record is in LDS (TStack::set_hit)
 };
 
 // Best.primpos flags: bit 31 = mixed-leaf ref position, bit 30 = the hit lies
@@ -579,6 +583,26 @@ __device__ __forceinline__ void resolve_inst(const DScene& sc, Best& b) {
 
 enum : int { TRAV_RUNNING = 0, TRAV_DONE = 1, TRAV_ANYHIT = 2 };
 
+// accept() on the split record: a hit was accepted iff bt < tmax (the first
+// acceptance needs t < tmax), and the tie rule reads the LDS words.
+__device__ __forceinline__ bool accept_hit(const DScene& sc, float t, int kind, int refpos, int primpos, const Trav& T,
+                                           const TStack& S) {
+  if (t < T.bt) return true;
+  if (t == T.bt && T.bt < T.tmax) return tie_wins(sc, kind, refpos, primpos, S.hit_kind(), S.hit_refpos(), S.hit_primpos());
+  return false;
+}
+__device__ __forceinline__ void take_hit(Trav& T, const TStack& S, float t, int kind, int idx, int refpos, int primpos) {
+  T.bt = t;
+  S.set_hit(kind, idx, refpos, primpos);
+}
+// The finished ray's record (inst resolved by the caller, resolve_inst).
+__device__ __forceinline__ Best trav_best(const Trav& T, const TStack& S) {
+  Best b;
+  b.t = T.bt; b.inst = -1;
+  b.kind = S.hit_kind(); b.idx = S.hit_idx(); b.refpos = S.hit_refpos(); b.primpos = S.hit_primpos();
+  return b;
+}
+
 // Set up one ray: planes (lifted out of the BVH) and the root box.
 template <bool kAny, bool kCount>
 __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack& S, V3 wo, V3 wd, float time,
@@ -586,16 +610,14 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
                                          Cnt& cnt) {
   T.time = time; T.tmin = tmin; T.tmax = tmax;
   T.key = key; T.bounce = bounce; T.voldom = voldom;
-  Best& best = T.best;
-  best.t = tmax; best.kind = 0; best.idx = -1; best.inst = -1; best.refpos = 0; best.primpos = 0;
+  T.bt = tmax;
+  if (!kAny) S.set_hit(0, -1, 0, 0);
   for (int i = 0; i < sc.num_planes; ++i) {
     float t = 0.0f;
     if (kCount) cnt.plane++;
     if (plane_t(sc.planes[i], wo, wd, tmin, t)) {
       if (kAny) { if (t < tmax) return TRAV_ANYHIT; }
-      else if (accept(sc, t, PK_PLANE, -1 - i, 0, best)) {
-        best.t = t; best.kind = PK_PLANE; best.idx = i; best.inst = -1; best.refpos = -1 - i; best.primpos = 0;
-      }
+      else if (accept_hit(sc, t, PK_PLANE, -1 - i, 0, T, S)) take_hit(T, S, t, PK_PLANE, i, -1 - i, 0);
     }
   }
   T.cr = make_tray(wo, wd);
@@ -605,7 +627,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
   float tn = 0.0f;
   if (sc.tlas.check_box &&
       !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
-               T.cr, tmin, kAny ? tmax : best.t, tn))
+               T.cr, tmin, kAny ? tmax : T.bt, tn))
     return TRAV_DONE;
   T.item = sc.tlas.root_item;
   if ((T.item >> ITEM_SHIFT) != ITEM_NODE) {
@@ -623,7 +645,6 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
 template <bool kAny, bool kCount, bool kVol>
 __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
-  Best& best = T.best;
   auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return S.pop(T.sp); };
   // The host bounds the stack need (flatten: stack_needed <= kStackMax), so an
   // overflow is an internal error: flagged for the host, the entry dropped,
@@ -666,7 +687,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t st1 = rtg_stamp();
 #endif
-    const float hi = kAny ? T.tmax : best.t;
+    const float hi = kAny ? T.tmax : T.bt;
     const float inf = __builtin_inff();
     auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
       const float tx0 = (nxp - T.cr.o.x) * T.cr.inv.x, tx1 = (fxp - T.cr.o.x) * T.cr.inv.x;
@@ -759,10 +780,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         if (kAny) { any = any || t <= T.tmax; return; }
         const int refpos = world ? pos : T.cur_ref;
         const int primpos = world ? 0 : (PRIM_IN_INST | pos);
-        if (accept(sc, t, PK_TRI, refpos, primpos, best)) {
-          best.t = t; best.kind = PK_TRI; best.idx = pos;
-          best.refpos = refpos; best.primpos = primpos;
-        }
+        if (accept_hit(sc, t, PK_TRI, refpos, primpos, T, S)) take_hit(T, S, t, PK_TRI, pos, refpos, primpos);
       };
       tri_one(DTri{{g0.x, g0.y, g0.z}, {g0.w, g1.x, g1.y}, {g1.z, g1.w, g2.x}}, int(idx));
       if (kAny && any) return TRAV_ANYHIT;
@@ -799,21 +817,18 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           const float4 lo = bp[0], hi = bp[1];
           float tn = 0.0f;
           if (kCount) cnt.ibox++;
-          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : best.t, tn)) continue;
+          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : T.bt, tn)) continue;
           push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos));
           continue;
         } else if (kVol && pk == PK_VOLUME) {
-          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), T.time, T.tmin, kAny ? T.tmax : best.t,
+          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), T.time, T.tmin, kAny ? T.tmax : T.bt,
                                   leaf_ntests(leaf.info), T.key, T.bounce, T.voldom, t, cnt);
         }
         if (!ok) continue;
         if (kAny) return TRAV_ANYHIT;
         const int refpos = world ? pos : T.cur_ref;
         const int primpos = world ? 0 : ((kind == PK_MIXED ? PRIM_MIXED : 0) | PRIM_IN_INST | pos);
-        if (accept(sc, t, pk, refpos, primpos, best)) {
-          best.t = t; best.kind = pk; best.idx = int(pi);
-          best.refpos = refpos; best.primpos = primpos;
-        }
+        if (accept_hit(sc, t, pk, refpos, primpos, T, S)) take_hit(T, S, t, pk, int(pi), refpos, primpos);
       }
     } else if (tag == ITEM_WQUAD || tag == ITEM_WSPHERE) {
       // a world leaf of one quad / sphere, inline in its node slot
@@ -841,10 +856,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       if (ok) {
         if (kAny) return TRAV_ANYHIT;
         const int refpos = pk == PK_QUAD ? sc.quad_wref[GIX(idx, sc.n_quads, 39)] : sc.sphere_wref[GIX(idx, sc.n_spheres, 49)];
-        if (accept(sc, t, pk, refpos, 0, best)) {
-          best.t = t; best.kind = pk; best.idx = int(idx);
-          best.refpos = refpos; best.primpos = 0;
-        }
+        if (accept_hit(sc, t, pk, refpos, 0, T, S)) take_hit(T, S, t, pk, int(idx), refpos, 0);
       }
     } else if (is_inst) {
       // One entry record per instance ref (DInstEntry, from the gather): for
@@ -853,7 +865,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       // several objects was culled there), then the wrapper chain (the ray
       // into object space, transform.go) and the BLAS root box.
       const bool winst = tag == ITEM_WINST;
-      const float hi = kAny ? T.tmax : best.t;
+      const float hi = kAny ? T.tmax : T.bt;
       float tn = 0.0f;
       bool go = true;
       if (winst) {
@@ -929,8 +941,8 @@ __device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin,
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   int s = trav_init<kAny, kCount>(sc, T, S, wo, wd, time, tmin, tmax, key, bounce, voldom, cnt);
   while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol>(sc, T, S, cnt, err);
-  best = T.best;
-  if (!kAny) resolve_inst(sc, best);
+  if (!kAny) { best = trav_best(T, S); resolve_inst(sc, best); }
+  else best = Best{};
   if (kAny) return s == TRAV_ANYHIT;
   return best.kind != 0;
 }

@@ -41,7 +41,7 @@ __global__ void tonemap_kernel(const float* accum, int n, int spp, uint8_t* rgba
 template <int STACK>
 __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, uint32_t seed, int sample,
                                                       int32_t* out_top, int32_t* out_prim, float* out_t, int* err) {
-  __shared__ uint32_t lds_stack[(STACK + 9) * 256];   // stack + world ray
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack + world ray
   const int tid = threadIdx.x;
   const int i = blockIdx.x * 256 + tid;
   if (i >= cam.width * cam.height) return;

@@ -29,19 +29,14 @@
 // 7 waves = 72 VGPRs).  The traversal is latency- and issue-bound, so
 // occupancy pays; measured on CornellBoxLucy (Msamples/s): 5 waves / 16-entry
 // LDS ring 681, 6 / 16 745, 7 / 8 757, 8 / 8 756 (64 B/lane of spills).  The
-// 8-entry ring + world ray (17 KB per block) lets LDS allow 9 blocks per CU.
+// 8-entry ring + world ray + hit record (21.5 KB per block in k_extend) lets
+// LDS hold the 7 blocks per CU that 7 waves/SIMD need.
 #ifndef RTG_TRAV_WAVES
 #define RTG_TRAV_WAVES 7
 #endif
 // The volume (fog) and instrumented variants carry more live state: at the
 // 96-VGPR cap they spill 40-120 VGPRs to scratch, so they keep 4 waves
 // (128 VGPRs) and compile without VGPR spills.
-// LDS words per lane beside the stack ring: the world ray (TStack::wr)
-#ifdef RTG_WORLD_RAY_REGS
-#define RTG_WR_WORDS 0
-#else
-#define RTG_WR_WORDS 9
-#endif
 #ifndef RTG_VOL_WAVES
 #define RTG_VOL_WAVES 4
 #endif
@@ -187,7 +182,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
                                                                 PathStream cs, const uint32_t* count,
                                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
                                                                 uint32_t* fetch, uint32_t sample_base) {
-  __shared__ uint32_t lds_stack[(STACK + RTG_WR_WORDS) * 256];   // stack ring + world ray
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack ring + world ray + hit record
   // next stream's count, the shadow job count and the shadow fetch counter
   if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
   const uint32_t n = *count;
@@ -214,7 +209,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       }
       const int s = trav_init<false, kCount>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), ray_time(asu(pd.w)),
                                              0.001f, __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
-      if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
+      if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
@@ -233,7 +228,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
     }
     if (p != ITEM_NONE) {
       const int s = trav_step<false, kCount, kVol>(sc, T, S, cnt, a.err);
-      if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, T.best); p = ITEM_NONE; }
+      if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
   }
 #ifdef RTG_STAMP
@@ -528,7 +523,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
 template <int STACK, bool kCount, bool kVol, bool kEnvIS>
 __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
-  __shared__ uint32_t lds_stack[(STACK + RTG_WR_WORDS) * 256];   // stack ring + world ray
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
   if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
