@@ -484,15 +484,19 @@ constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the sta
 // The lane's world-space ray (origin, direction, 1/direction) lives beside it
 // in LDS: it is read only on instance entry / exit and volume tests, so it
 // need not occupy nine VGPRs for the whole traversal.
-// The closest-hit record's identity (kind, index, ref / prim positions) sits
-// there too: it is written when a hit is accepted and read only on exact-t
-// ties and when the ray ends, so only the hit distance stays in a register.
+// So do the ray time (read only by moving-sphere and volume tests) and the
+// TLAS ref of the instance being traversed (read when a hit inside it is
+// accepted, written on instance entry / exit).
+// The closest-hit record's identity (kind<<28 | index, ref / prim positions)
+// sits there too: it is written when a hit is accepted and read only on
+// exact-t ties and when the ray ends, so only the hit distance stays in a
+// register.
 // Only `lds` is per lane (one VGPR); the rest is block-uniform: the lane's
 // spill column is spill_blk + (its LDS slot - lds0), formed on the rare
-// spill path, the world ray sits at lds + cap * stride and the hit record
-// after it.
-constexpr int kWorldRayWords = 9;   // LDS words per lane: world ray
-constexpr int kHitWords = 4;        // LDS words per lane: hit record (closest-hit kernels)
+// spill path, the ray words sit at lds + cap * stride and the hit record
+// after them.
+constexpr int kWorldRayWords = 11;  // LDS words per lane: world ray (9), time, current instance ref
+constexpr int kHitWords = 3;        // LDS words per lane: hit record (closest-hit kernels)
 struct TStack {
   uint32_t* lds;       // this lane's slot 0
   int stride;          // LDS words between slots (lanes interleaved)
@@ -520,15 +524,19 @@ struct TStack {
     const float* wr = wrp();
     return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]);
   }
+  __device__ __forceinline__ float time() const { return wrp()[9 * stride]; }
+  __device__ __forceinline__ void set_time(float t) const { wrp()[9 * stride] = t; }
+  __device__ __forceinline__ int cur_ref() const { return reinterpret_cast<const int*>(wrp())[10 * stride]; }
+  __device__ __forceinline__ void set_cur_ref(int r) const { reinterpret_cast<int*>(wrp())[10 * stride] = r; }
   __device__ __forceinline__ int* hitp() const { return reinterpret_cast<int*>(lds + (cap + kWorldRayWords) * stride); }
   __device__ __forceinline__ void set_hit(int kind, int idx, int refpos, int primpos) const {
     int* h = hitp();
-    h[0] = kind; h[stride] = idx; h[2 * stride] = refpos; h[3 * stride] = primpos;
+    h[0] = int((uint32_t(kind) << 28) | (uint32_t(idx) & 0x0FFFFFFFu)); h[stride] = refpos; h[2 * stride] = primpos;
   }
-  __device__ __forceinline__ int hit_kind() const { return hitp()[0]; }
-  __device__ __forceinline__ int hit_idx() const { return hitp()[stride]; }
-  __device__ __forceinline__ int hit_refpos() const { return hitp()[2 * stride]; }
-  __device__ __forceinline__ int hit_primpos() const { return hitp()[3 * stride]; }
+  __device__ __forceinline__ int hit_kind() const { return int(uint32_t(hitp()[0]) >> 28); }
+  __device__ __forceinline__ int hit_idx() const { return hitp()[0] & 0x0FFFFFFF; }
+  __device__ __forceinline__ int hit_refpos() const { return hitp()[stride]; }
+  __device__ __forceinline__ int hit_primpos() const { return hitp()[2 * stride]; }
 #ifdef RTG_RING24
   // diagnostic build only: a 24-entry ring is not a power of two
   __device__ __forceinline__ int ring(int sp) const { return int(uint32_t(sp) % uint32_t(cap)); }
@@ -565,10 +573,13 @@ __device__ __forceinline__ TStack lds_stack_only(uint32_t* lds, int stride, int 
 // The world-space ray is kept in the TStack's LDS area (TStack::wr).
 struct Trav {
   TRay cr;               // current-space ray (object space inside an instance)
-  float time, tmin, tmax;
+  // tmin / tmax default to the values every closest-hit ray uses (0.001, +inf,
+  // camera.go:462): a kernel that never sets other values keeps them as
+  // constants instead of loop-carried registers
+  float tmin = 0.001f, tmax = __builtin_inff();
   uint32_t key, bounce, voldom;
   uint32_t item, lf;
-  int sp, cur_ref;       // cur_ref: TLAS ref of the instance being traversed, -1 in world space
+  int sp;                // the ray time and the current instance ref are in LDS (TStack)
   float bt;              // closest accepted hit distance (tmax: none); the rest of the
                          // hit record is in LDS (TStack::set_hit)
 };
@@ -608,7 +619,7 @@ template <bool kAny, bool kCount>
 __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack& S, V3 wo, V3 wd, float time,
                                          float tmin, float tmax, uint32_t key, uint32_t bounce, uint32_t voldom,
                                          Cnt& cnt) {
-  T.time = time; T.tmin = tmin; T.tmax = tmax;
+  S.set_time(time); T.tmin = tmin; T.tmax = tmax;
   T.key = key; T.bounce = bounce; T.voldom = voldom;
   T.bt = tmax;
   if (!kAny) S.set_hit(0, -1, 0, 0);
@@ -622,7 +633,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
   }
   T.cr = make_tray(wo, wd);
   S.save_world(wo, wd, T.cr.inv);
-  T.cur_ref = -1; T.sp = 0;
+  S.set_cur_ref(-1); T.sp = 0;
   T.item = ITEM_NONE; T.lf = ITEM_NONE;
   float tn = 0.0f;
   if (sc.tlas.check_box &&
@@ -725,7 +736,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     }
     // leaving an instance with nothing postponed: restore the world ray inline
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END && T.lf == ITEM_NONE) {
-      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
+      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
@@ -771,14 +782,15 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       // come from the gather, any further ones (reference-topology leaves)
       // are loaded one at a time
       const int n = int(tag - ITEM_TRI1) + 1;
-      const bool world = T.cur_ref < 0;
       bool any = false;
       auto tri_one = [&](const DTri& tr, int pos) {
         float t = 0.0f;
         if (kCount) cnt.tri++;
         if (!tri_t(tr, T.cr.o, T.cr.d, T.tmin, t)) return;
         if (kAny) { any = any || t <= T.tmax; return; }
-        const int refpos = world ? pos : T.cur_ref;
+        const int cref = S.cur_ref();
+        const bool world = cref < 0;
+        const int refpos = world ? pos : cref;
         const int primpos = world ? 0 : (PRIM_IN_INST | pos);
         if (accept_hit(sc, t, PK_TRI, refpos, primpos, T, S)) take_hit(T, S, t, PK_TRI, pos, refpos, primpos);
       };
@@ -790,7 +802,6 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     } else if (tag == ITEM_LEAF) {
       const DLeaf leaf{__float_as_uint(g0.x), __float_as_uint(g0.y)};
       const int n = leaf_count(leaf.info), kind = leaf_kind(leaf.info);
-      const bool world = T.cur_ref < 0;
       for (int k = 0; k < n; ++k) {
         int pk = kind;
         uint32_t pi = leaf.first + k;
@@ -806,7 +817,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           ok = quad_t(sc.quads[GIX(pi, sc.n_quads, 13)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
         } else if (pk == PK_SPHERE) {
           if (kCount) cnt.sph++;
-          ok = sphere_t(sc.spheres[GIX(pi, sc.n_spheres, 14)], T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+          ok = sphere_t(sc.spheres[GIX(pi, sc.n_spheres, 14)], T.cr.o, T.cr.d, S.time(), T.tmin, t) && (kAny ? t < T.tmax : true);
         } else if (kVol && pk == PK_CIRCLE) {   // kVol: the rare-primitive variant (volumes, circles)
           if (kCount) cnt.quad++;   // counted with the quads (same kind of test)
           ok = circle_t(sc.circles[GIX(pi, sc.n_circles, 34)], T.cr.o, T.cr.d, T.tmin, t) && (kAny ? t <= T.tmax : true);
@@ -821,12 +832,14 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos));
           continue;
         } else if (kVol && pk == PK_VOLUME) {
-          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), T.time, T.tmin, kAny ? T.tmax : T.bt,
+          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), S.time(), T.tmin, kAny ? T.tmax : T.bt,
                                   leaf_ntests(leaf.info), T.key, T.bounce, T.voldom, t, cnt);
         }
         if (!ok) continue;
         if (kAny) return TRAV_ANYHIT;
-        const int refpos = world ? pos : T.cur_ref;
+        const int cref = S.cur_ref();
+        const bool world = cref < 0;
+        const int refpos = world ? pos : cref;
         const int primpos = world ? 0 : ((kind == PK_MIXED ? PRIM_MIXED : 0) | PRIM_IN_INST | pos);
         if (accept_hit(sc, t, pk, refpos, primpos, T, S)) take_hit(T, S, t, pk, int(pi), refpos, primpos);
       }
@@ -851,7 +864,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         DSphere sp;
         sp.cx = g0.x; sp.cy = g0.y; sp.cz = g0.z; sp.r = g0.w;
         sp.vx = g1.x; sp.vy = g1.y; sp.vz = g1.z; sp.mat = 0;
-        ok = sphere_t(sp, T.cr.o, T.cr.d, T.time, T.tmin, t) && (kAny ? t < T.tmax : true);
+        ok = sphere_t(sp, T.cr.o, T.cr.d, S.time(), T.tmin, t) && (kAny ? t < T.tmax : true);
       }
       if (ok) {
         if (kAny) return TRAV_ANYHIT;
@@ -896,12 +909,12 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         if (enter) {
           if (T.item < ITEM_POP) push(T.item);
           push(ITEM_INST_END << ITEM_SHIFT);
-          T.cr = orr; T.cur_ref = int(idx);
+          T.cr = orr; S.set_cur_ref(int(idx));
           T.item = __float_as_uint(g2.w);   // BLAS root item
         }
       }
     } else {  // ITEM_INST_END: back to the world-space ray
-      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
+      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
     }
 #ifdef RTG_STAMP
     const uint32_t sb = rtg_stamp();
@@ -912,7 +925,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     if (T.item == ITEM_POP || T.item == ITEM_NONE) T.item = pop();
     // leaving an instance: restore the world ray here, not in another round
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END) {
-      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); T.cur_ref = -1;
+      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE) postpone();
@@ -1187,7 +1200,12 @@ __device__ __forceinline__ V3 disk_point(uint32_t key) {   // RandomInUnitDisk (
   return p;
 }
 
-__device__ __noinline__ void get_ray_slow(const DCamera& cam, int px, int py, uint32_t key, float offx, float offy,
+#ifdef RTG_INLINE_SLOW_CAMERA
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void get_ray_slow(const DCamera& cam, int px, int py, uint32_t key, float offx, float offy,
                                           float time, V3& ro, V3& rd) {
   V3 center = add(ld3(cam.c_orig), scale(ld3(cam.c_dir), time));          // centerMotion.At(rayTime)
   V3 w;

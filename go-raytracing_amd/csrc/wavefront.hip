@@ -153,7 +153,8 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
     const int leader = __ffsll(m) - 1;
     uint32_t base = 0;
     if (__lane_id() == leader) base = atomicAdd(ctr, run);
-    base = __shfl(base, leader);
+    // wave-uniform: scalar registers for the pool state
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
     if (base >= n) { P.dry = true; return ITEM_NONE; }
     P.cur = base;
     P.end = n - base > run ? base + run : n;
@@ -549,7 +550,9 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   // ray r of the current job ended with status s; true when the job is done
   auto advance = [&](int s) -> bool {
     if (s != TRAV_ANYHIT) vis |= r == 0 ? 2u : 1u;
-    if (r == 0 && (info & 1u)) {
+    // (kEnvIS: only then can a job start with its HDRI ray; without it the
+    // job's origin and area direction are dead once its one ray started)
+    if (kEnvIS && r == 0 && (info & 1u)) {
       r = 1;
       const int s2 = start_ray(1, mk(da.x, da.y, da.z), da.w);
       if (s2 == TRAV_RUNNING) return false;

@@ -41,6 +41,7 @@ inline int __lane_id() { return 0; }
 inline unsigned long long __ballot(bool p) { return p ? 1ull : 0ull; }
 template <class T>
 inline T __shfl(T v, int) { return v; }
+inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return v; }
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 inline int __ffsll(unsigned long long x) { return __builtin_ffsll(static_cast<long long>(x)); }
 inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { const uint32_t o = *p; *p = o + v; return o; }
