@@ -44,24 +44,25 @@ sys.path.insert(0, ROOT)
 
 # Algorithmic bytes per unit of work.
 BYTES = {
-    "node_visits": 128,      # one BVH4 node = four 24-B child boxes + four child items
+    "node_visits": 128,      # one BVH4 node (DNode4): four 24-B child boxes + four child items (64 B with --nodes quant8)
     "tri_tests": 36,         # v0, e1, e2 fp32
     "sphere_tests": 32,
     "quad_tests": 64,
     "plane_tests": 32,
-    "instance_visits": 96,   # 3x4 affine + inverse (SURVEY: 96 B)
+    "instance_visits": 112,  # instance entry gather: wrappers 0-2 + BLAS root item and box (SURVEY: 96 B)
     "instance_box_tests": 32,  # world-space instance culling box
     "volume_tests": 64,
     "material_fetches": 32,
     "env_lookups": 48,       # 4 texels x 12 B
 }
 # Path-stream bytes per unit.
-EXTEND_RAY_IO = 48           # ray o, d in (32) + hit record out (16); +16 (throughput word) with volumes
-SHADE_PATH_IN = 80           # hit, o, d, throughput, L of every shaded path
-SHADE_SURVIVOR_OUT = 64      # o, d, throughput, L of the next stream
-SHADE_END_OUT = 16           # Lout of an ended path (once per sample)
-SHADE_JOB_OUT = 68           # NEE job: origin, area dir, info, contribution, throughput (+32 with HDRI IS)
-SHADOW_JOB_IO = 40           # job origin, area dir, info in, visibility out (+16 with HDRI IS)
+EXTEND_RAY_IO = 48           # ray o, d in (32) + hit record out (16); +16 (throughput word) with volumes;
+                             # bounce 0 regenerates the camera ray (hit out only)
+SHADE_PATH_IN = 64           # hit, o, d, throughput of a shaded path (bounce 0: the hit only, 16)
+SHADE_SURVIVOR_OUT = 48      # o, d, throughput of the next stream
+SHADE_END_OUT = 16           # Lout of a sample, zeroed / set at bounce 0 (emission adds later are not counted)
+SHADE_JOB_OUT = 52           # NEE job: origin, area dir, info, contribution (+48 with HDRI IS: dir, contribution, throughput)
+SHADOW_JOB_IO = 36           # job origin, area dir in, visibility out (+20 with HDRI IS: dir, info)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 # BASELINE.json configs run on the GPU (C1 SimpleScene is the CPU plumbing case).
@@ -84,6 +85,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=0, help="0: scene default")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--nodes", choices=["fp32", "quant8"], default="fp32",
+                    help="BVH4 node format (RT_OPT_NODE_FORMAT)")
     ap.add_argument("--blas", choices=["sah", "reference", "device"], default="sah",
                     help="mesh BLAS builder: host SAH (default), the caller's topology, or the GPU LBVH "
                          "(build.hip); the world BVH is SAH except for 'reference'")
@@ -173,7 +176,7 @@ class Dist:
 class Workload:
     """One scene resident on this rank's GPU, this rank's bucket shard."""
 
-    def __init__(self, g, D: Dist, scene: str, scene_kw: dict, seed: int, blas: str):
+    def __init__(self, g, D: Dist, scene: str, scene_kw: dict, seed: int, blas: str, nodes: str = "fp32"):
         import torch
         self.g, self.D = g, D
         t = time.time()
@@ -184,6 +187,8 @@ class Workload:
         self.ctx = g.Context(D.dev_index)
         self.ctx.set_blas_builder(blas)
         self.ctx.set_tlas_builder("reference" if blas == "reference" else "sah")
+        if nodes != "fp32":   # fp32 is the default format
+            self.ctx.set_node_format(nodes)
         self.ctx.upload(self.scene.desc)
         self.info = self.ctx.info()
         self.dev_build_ms = self.ctx.last_build_ms()
@@ -252,10 +257,10 @@ def kernel_report(w: Workload, work_k: dict, pmc: dict | None):
     samples = ext["samples"]
     trav = {k: sum(BYTES[u] * wk[u] for u in BYTES) for k, wk in (("extend", ext), ("shade", sha), ("shadow", shd))}
     alg = {
-        "extend": trav["extend"] + (EXTEND_RAY_IO + (16 if vol else 0)) * ext["rays"],
-        "shade": trav["shade"] + SHADE_PATH_IN * sha["rays"] + SHADE_SURVIVOR_OUT * (ext["rays"] - samples)
-                 + SHADE_END_OUT * samples + (SHADE_JOB_OUT + (32 if envis else 0)) * sha["shadow_rays"],
-        "shadow": trav["shadow"] + (SHADOW_JOB_IO + (16 if envis else 0)) * sha["shadow_rays"],
+        "extend": trav["extend"] + (EXTEND_RAY_IO + (16 if vol else 0)) * ext["rays"] - 32 * samples,
+        "shade": trav["shade"] + SHADE_PATH_IN * sha["rays"] - 48 * samples + SHADE_SURVIVOR_OUT * (ext["rays"] - samples)
+                 + SHADE_END_OUT * samples + (SHADE_JOB_OUT + (48 if envis else 0)) * sha["shadow_rays"],
+        "shadow": trav["shadow"] + (SHADOW_JOB_IO + (20 if envis else 0)) * sha["shadow_rays"],
     }
     out = {}
     for k in ("extend", "shade", "shadow"):
@@ -297,7 +302,9 @@ def main():
         scene_kw["spp"] = args.spp
     if args.depth:
         scene_kw["max_depth"] = args.depth
-    w = Workload(g, D, args.scene, scene_kw, args.seed, args.blas)
+    if args.nodes == "quant8":
+        BYTES["node_visits"] = 64   # one DNodeQ
+    w = Workload(g, D, args.scene, scene_kw, args.seed, args.blas, args.nodes)
     W, H, spp, depth = w.W, w.H, w.spp, w.depth
 
     # one HIP event before each extend/shade/shadow launch (and after each
@@ -374,7 +381,7 @@ def main():
                 configs[cid] = {"workload": f"{scene} {W}x{H} {spp}spp depth {depth}", "value": round(value, 3),
                                 "ms_per_step": round(ms_per_step, 3), "steps": args.steps, "frame_sum": frame_sum}
                 continue
-            cw = Workload(g, D, scene, kw, args.seed, args.blas)
+            cw = Workload(g, D, scene, kw, args.seed, args.blas, args.nodes)
             el = cw.run(args.config_steps, 1)
             configs[cid] = {"workload": f"{scene} {cw.W}x{cw.H} {cw.spp}spp depth {cw.depth}",
                             "value": round(cw.samples() * args.config_steps / el / 1e6, 3),
@@ -417,7 +424,7 @@ def main():
             "data": "synthetic (deterministic 280K-tri Lucy stand-in; scene geometry per scenes.go)",
             "config": {"workload": f"{args.scene} {W}x{H} {spp}spp depth {depth}", "scene": args.scene,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "parallelism": f"tiles-rr{D.world}", "buckets": len(w.buckets), "blas": args.blas,
+                       "parallelism": f"tiles-rr{D.world}", "buckets": len(w.buckets), "blas": args.blas, "nodes": args.nodes,
                        "triangles": w.info.triangles, "bvh_nodes": w.info.nodes,
                        "scene_build_s": round(w.build_s, 2), "device_bvh_build_ms": round(w.dev_build_ms, 2),
                        "image_finite": img_ok, "frame_sum": frame_sum},

@@ -28,8 +28,9 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 ASSET_DIR = os.path.join(REPO_DIR, "assets")
 
 RT_OK = 0
-RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER = 1, 2
+RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER, RT_OPT_NODE_FORMAT = 1, 2, 3
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
+RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_SCENE", -6: "RT_ERR_DEVICE"}
 
@@ -430,6 +431,11 @@ class Context:
     def set_tlas_builder(self, builder: str):
         """World BVH layout: "sah" (default) or "reference"; next upload."""
         self.set_option(RT_OPT_TLAS_BUILDER, {"reference": RT_BLAS_REFERENCE, "sah": RT_BLAS_SAH}[builder])
+
+    def set_node_format(self, fmt: str):
+        """BVH4 node records: "fp32" (default, 128 B) or "quant8" (64 B,
+        8-bit child planes with a conservative margin); next upload."""
+        self.set_option(RT_OPT_NODE_FORMAT, {"fp32": RT_NODES_FP32, "quant8": RT_NODES_QUANT8}[fmt])
 
     def set_kernel_timing(self, enable: bool = True):
         self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))

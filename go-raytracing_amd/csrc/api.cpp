@@ -481,6 +481,11 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
     ctx->fopt.tlas_builder = value == RT_BLAS_SAH ? BLAS_SAH : BLAS_REFERENCE;
     return RT_OK;
   }
+  if (key == RT_OPT_NODE_FORMAT) {
+    if (value != RT_NODES_FP32 && value != RT_NODES_QUANT8) return set_err(ctx, RT_ERR_INVALID, "bad node format");
+    ctx->fopt.quant_nodes = value == RT_NODES_QUANT8 ? 1 : 0;
+    return RT_OK;
+  }
   return set_err(ctx, RT_ERR_INVALID, "unknown option " + std::to_string(key));
 }
 
@@ -599,6 +604,7 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed;
   d.has_volumes = h.volumes.empty() ? 0 : 1;
+  d.quant_nodes = h.quant_nodes;
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
@@ -613,6 +619,16 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;
   if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }
+  // RT_NODES_QUANT8: the traversal's quantised nodes, from every final node
+  // (host + device built)
+  if (d.quant_nodes) {
+    if ((rc = upload_vec(ctx, std::vector<DNodeQ>(), &d.qnodes, d.n_nodes))) { free_scene(ctx); return rc; }
+    if (hipError_t qe = quantize_nodes(d.nodes, const_cast<DNodeQ*>(d.qnodes), d.n_nodes, ctx->stream)) {
+      rc = hip_fail(ctx, qe, "node quantisation");
+      free_scene(ctx);
+      return rc;
+    }
+  }
   build_inst_entries(h);   // BLAS roots are final now
   if ((rc = upload_vec(ctx, h.inst_entries, &d.inst_entry))) { free_scene(ctx); return rc; }
   ctx->has_scene = true;

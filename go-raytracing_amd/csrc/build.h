@@ -44,4 +44,8 @@ struct DeviceBuildResult {
 hipError_t build_mesh_blas(const DeviceBuildJob& job, const DRefBox* boxes, DeviceBuildTarget& tgt,
                            DeviceBuildResult& res, hipStream_t st);
 
+// The traversal's quantised node array (node_quant.h) from the build form:
+// out[i] = quantize_node(in[i]) for i < n.  Synchronous on `st`.
+hipError_t quantize_nodes(const DNode4* in, DNodeQ* out, uint32_t n, hipStream_t st);
+
 }  // namespace rtg

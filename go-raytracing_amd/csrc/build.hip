@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "build.h"
+#include "node_quant.h"
 
 namespace rtg {
 namespace {
@@ -202,6 +203,13 @@ __global__ __launch_bounds__(256) void k_gather(const T* src, T* dst, const uint
   if (i < n) dst[i] = src[vals[i]];
 }
 
+// DNode4 -> DNodeQ for every node (host-built and device-built alike),
+// after the device builds: the traversal reads only the quantised form.
+__global__ __launch_bounds__(256) void k_quantize(const DNode4* in, DNodeQ* out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = quantize_node(in[i]);
+}
+
 // Device scratch of one build, freed on every exit path.
 struct Scratch {
   std::vector<void*> ptrs;
@@ -321,6 +329,13 @@ hipError_t build_mesh_blas(const DeviceBuildJob& job, const DRefBox* boxes, Devi
   res.leaves_added = fin[1];
   res.need4 = int(fin[3]);
   return hipSuccess;
+}
+
+hipError_t quantize_nodes(const DNode4* in, DNodeQ* out, uint32_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_quantize, dim3(blocks(n)), dim3(256), 0, st, in, out, n);
+  BCHK(hipGetLastError());
+  return hipStreamSynchronize(st);
 }
 
 }  // namespace rtg

@@ -96,11 +96,31 @@ struct alignas(16) DNode4 {
   uint32_t item[4];
   uint32_t pad[4];
 };
-// The traversal addresses nodes by 32-bit byte offset (index << 7): at most
-// 2^25 BVH4 nodes per scene (flatten / device_builds refuse more).
+// At most 2^25 BVH4 nodes per scene (flatten / device_builds refuse more):
+// the traversal addresses the quantised nodes by 32-bit byte offset
+// (index << 6), and the build form stays addressable the same way.
 constexpr uint32_t kMaxNodes4 = 1u << 25;
 static_assert(sizeof(DNode4) == 128 && uint64_t(kMaxNodes4) * sizeof(DNode4) == (uint64_t(1) << 32),
               "32-bit node byte offsets");
+
+// Quantised BVH4 node, 64 B (two per L2 line): what the traversal reads.
+// Each axis has a node frame (origin, step); a child's planes are 8-bit step
+// counts from the origin, rounded outward beyond the fp32 DNode4 box by a
+// margin that covers the slab test's rounding (node_quant.h), so every test
+// stays conservative and hits are unchanged (boxes only cull; the DFS tie
+// rule does not depend on the visiting order).  The slab test evaluates the
+// plane's t as fma(q, inv * step, (origin - o) * inv): one convert + one fma
+// per plane, the same VALU count as (plane - o) * inv.
+//   q[0..5] = rows xlo, xhi, ylo, yhi, zlo, zhi; byte c of a row = child c.
+//   An unused child has lo = 255, hi = 0 on every axis (rejected by any
+//   finite slab).
+struct alignas(64) DNodeQ {
+  float org[3];      // per-axis frame origin
+  float step[3];     // per-axis step
+  uint32_t q[6];
+  uint32_t item[4];  // child items, as DNode4
+};
+static_assert(sizeof(DNodeQ) == 64, "DNodeQ: half an L2 line");
 
 struct alignas(8) DLeaf {
   uint32_t first;  // index into refs (PK_MIXED) or into the kind's prim array
@@ -252,7 +272,8 @@ struct alignas(16) DRefBox {
 
 // Everything the kernels need, passed by value as a kernel argument.
 struct DScene {
-  const DNode4* nodes;         // BVH4 nodes (ITEM_NODE indexes this array)
+  const DNode4* nodes;         // BVH4 nodes, full fp32 boxes (build form; ITEM_NODE indexes it)
+  const DNodeQ* qnodes;        // the same nodes quantised (RT_NODES_QUANT8; else null)
   const DLeaf* leaves;
   const uint32_t* refs;
   const int32_t* ref_rank;     // DFS rank of each TLAS ref (tie rule)
@@ -298,6 +319,7 @@ struct DScene {
   int32_t has_volumes;
   int32_t has_fancy;      // a Metal / Dielectric / Isotropic material exists
   int32_t needs_uv;       // an ImageTexture exists: hit records carry U/V
+  int32_t quant_nodes;    // traverse the quantised DNodeQ nodes (RT_NODES_QUANT8), else DNode4
   // array lengths (bounds checks of the RTG_GUARD diagnostic build)
   uint32_t n_nodes, n_leaves, n_refs, n_spheres, n_quads, n_tris, n_instances, n_blas, n_volumes, n_circles;
 };

@@ -654,7 +654,8 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
 // independent of visiting order (BVHNode.Hit bvh.go:219-239 is left-first).
 //   kAny = false: closest hit in [tmin, tmax) with the tie rule.
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
-template <bool kAny, bool kCount, bool kVol>
+//   kQuant = true: the node records are DNodeQ (RT_NODES_QUANT8), else DNode4.
+template <bool kAny, bool kCount, bool kVol, bool kQuant = false>
 __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
   auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return S.pop(T.sp); };
   // The host bounds the stack need (flatten: stack_needed <= kStackMax), so an
@@ -675,43 +676,86 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const bool st_lead = rtg_lead();
     const uint32_t st0 = rtg_stamp();
 #endif
-    // 32-bit byte offsets from the uniform node base (saddr + voffset loads)
-    const uint32_t nb = GIX(T.item & ITEM_MASK, sc.n_nodes, 9) << 7;
-    const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
-    auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };
-    // box_hit for the four children at once: the near / far plane of each
-    // axis is picked by the load address (the ray's direction signs) instead
-    // of per-child selects — the same operations as box_hit, bit for bit.
-    const uint32_t sxo = (__float_as_uint(T.cr.inv.x) >> 27) & 16u, syo = (__float_as_uint(T.cr.inv.y) >> 27) & 16u,
-                   szo = (__float_as_uint(T.cr.inv.z) >> 27) & 16u;
-    const float4 nx = ldn(nb + sxo), fx = ldn(nb + (16u - sxo)), ny = ldn(nb + (32u + syo)), fy = ldn(nb + (48u - syo));
-    const float4 nz = ldn(nb + (64u + szo)), fz = ldn(nb + (80u - szo));
-    const uint4 it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
-#if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
-    // issue the child-item load with the plane loads (same 128-B line): the
-    // compiler otherwise sinks it into the "a child was hit" branch, which
-    // costs a second dependent round trip per node
-    asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));
-#endif
-    if (kCount) cnt.nodes++;
-#ifdef RTG_STAMP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t st1 = rtg_stamp();
-#endif
     const float hi = kAny ? T.tmax : T.bt;
     const float inf = __builtin_inff();
-    auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
-      const float tx0 = (nxp - T.cr.o.x) * T.cr.inv.x, tx1 = (fxp - T.cr.o.x) * T.cr.inv.x;
-      const float ty0 = (nyp - T.cr.o.y) * T.cr.inv.y, ty1 = (fyp - T.cr.o.y) * T.cr.inv.y;
-      const float tz0 = (nzp - T.cr.o.z) * T.cr.inv.z, tz1 = (fzp - T.cr.o.z) * T.cr.inv.z;
+    const uint32_t nidx = GIX(T.item & ITEM_MASK, sc.n_nodes, 9);
+    float t0, t1, t2, t3;
+    uint4 it;
+    // the slab test of the four children: returns the entry t, or +inf
+    auto slab = [&](float tx0, float tx1, float ty0, float ty1, float tz0, float tz1) {
       const float a = fmaxf(fmaxf(fmaxf(T.tmin, tx0), ty0), tz0);
       const float b = fminf(fminf(fminf(hi, tx1), ty1), tz1);
       return b > a ? a : inf;
     };
-    float t0 = child_t(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x);
-    float t1 = child_t(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y);
-    float t2 = child_t(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z);
-    float t3 = child_t(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w);
+    if (kQuant) {
+      // Quantised node (DNodeQ, 64 B; 32-bit byte offsets from the uniform
+      // node base, saddr + voffset loads).  Each child box holds its fp32
+      // DNode4 box with a margin (node_quant.h), so the test is conservative.
+      // Per axis, a plane q steps from the frame origin is at
+      // t = fma(q, inv * step, (origin - o) * inv); the near / far row is
+      // picked by the direction's sign.  An infinite 1/d gives NaN or +-inf
+      // planes, which fmaxf / fminf ignore or keep: that axis culls nothing.
+      const uint32_t nb = nidx << 6;
+      const char* const nbase = reinterpret_cast<const char*>(sc.qnodes);
+      const float4 f0 = *reinterpret_cast<const float4*>(nbase + nb);            // org xyz, step x
+      const float4 f1 = *reinterpret_cast<const float4*>(nbase + (nb + 16u));    // step yz, xlo xhi rows
+      const uint4 ryz = *reinterpret_cast<const uint4*>(nbase + (nb + 32u));     // ylo yhi zlo zhi rows
+      it = *reinterpret_cast<const uint4*>(nbase + (nb + 48u));
+#if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
+      // issue the child-item load with the plane loads (same line): the
+      // compiler otherwise sinks it into the "a child was hit" branch, which
+      // costs a second dependent round trip per node
+      asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));
+#endif
+#ifdef RTG_STAMP
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      const float ax = (f0.x - T.cr.o.x) * T.cr.inv.x, bx = T.cr.inv.x * f0.w;
+      const float ay = (f0.y - T.cr.o.y) * T.cr.inv.y, by = T.cr.inv.y * f1.x;
+      const float az = (f0.z - T.cr.o.z) * T.cr.inv.z, bz = T.cr.inv.z * f1.y;
+      const bool sx = (__float_as_uint(T.cr.inv.x) >> 31) != 0u, sy = (__float_as_uint(T.cr.inv.y) >> 31) != 0u,
+                 sz = (__float_as_uint(T.cr.inv.z) >> 31) != 0u;
+      const uint32_t xlo = __float_as_uint(f1.z), xhi = __float_as_uint(f1.w);
+      const uint32_t nqx = sx ? xhi : xlo, fqx = sx ? xlo : xhi;
+      const uint32_t nqy = sy ? ryz.y : ryz.x, fqy = sy ? ryz.x : ryz.y;
+      const uint32_t nqz = sz ? ryz.w : ryz.z, fqz = sz ? ryz.z : ryz.w;
+      auto child_t = [&](int c) {
+        auto qf = [c](uint32_t row) { return float((row >> (8 * c)) & 0xFFu); };   // v_cvt_f32_ubyte<c>
+        return slab(fmaf(qf(nqx), bx, ax), fmaf(qf(fqx), bx, ax), fmaf(qf(nqy), by, ay), fmaf(qf(fqy), by, ay),
+                    fmaf(qf(nqz), bz, az), fmaf(qf(fqz), bz, az));
+      };
+      t0 = child_t(0); t1 = child_t(1); t2 = child_t(2); t3 = child_t(3);
+    } else {
+      // Full fp32 boxes (DNode4, 128 B; the default node format): the near /
+      // far plane of each axis is picked by the load address (the
+      // direction's signs) instead of per-child selects: box_hit, bit for bit.
+      const uint32_t nb = nidx << 7;
+      const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
+      auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };
+      const uint32_t sxo = (__float_as_uint(T.cr.inv.x) >> 27) & 16u, syo = (__float_as_uint(T.cr.inv.y) >> 27) & 16u,
+                     szo = (__float_as_uint(T.cr.inv.z) >> 27) & 16u;
+      const float4 nx = ldn(nb + sxo), fx = ldn(nb + (16u - sxo)), ny = ldn(nb + (32u + syo)), fy = ldn(nb + (48u - syo));
+      const float4 nz = ldn(nb + (64u + szo)), fz = ldn(nb + (80u - szo));
+      it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
+#if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
+      asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));   // as above
+#endif
+#ifdef RTG_STAMP
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
+        return slab((nxp - T.cr.o.x) * T.cr.inv.x, (fxp - T.cr.o.x) * T.cr.inv.x, (nyp - T.cr.o.y) * T.cr.inv.y,
+                    (fyp - T.cr.o.y) * T.cr.inv.y, (nzp - T.cr.o.z) * T.cr.inv.z, (fzp - T.cr.o.z) * T.cr.inv.z);
+      };
+      t0 = child_t(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x);
+      t1 = child_t(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y);
+      t2 = child_t(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z);
+      t3 = child_t(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w);
+    }
+    if (kCount) cnt.nodes++;
+#ifdef RTG_STAMP
+    const uint32_t st1 = rtg_stamp();
+#endif
     // near-to-far order (5-comparator network, missed children sort last as
     // +inf); visit the nearest, push the other hit children far first
     uint32_t i0 = it.x, i1 = it.y, i2 = it.z, i3 = it.w;
@@ -947,13 +991,13 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
 }
 
 // Whole-ray traversal (probe kernel, megakernel).
-template <bool kAny, bool kCount, bool kVol = true>
+template <bool kAny, bool kCount, bool kVol = true, bool kQuant = false>
 __device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin, float tmax,
                          const TStack& S, Best& best, uint32_t key,
                          uint32_t bounce, uint32_t voldom, Cnt& cnt, int* err) {
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   int s = trav_init<kAny, kCount>(sc, T, S, wo, wd, time, tmin, tmax, key, bounce, voldom, cnt);
-  while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol>(sc, T, S, cnt, err);
+  while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol, kQuant>(sc, T, S, cnt, err);
   if (!kAny) { best = trav_best(T, S); resolve_inst(sc, best); }
   else best = Best{};
   if (kAny) return s == TRAV_ANYHIT;

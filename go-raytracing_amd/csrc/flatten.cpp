@@ -1132,6 +1132,10 @@ struct Flattener {
     // in a leaf + the pending item and INST_END marker of an instance entry +
     // pending siblings along the worst BLAS path.
     S.max_leaf_inst = max_leaf_inst;
+    // RotateX/RotateZ bboxes do not contain what Hit sees (transform.go:201-351):
+    // which rays reach those objects depends on the exact node boxes, so such
+    // scenes keep the fp32 DNode4 boxes whatever node format was asked for
+    S.quant_nodes = opt.quant_nodes && tlas_sah_ok() ? 1 : 0;
     S.stack_needed = S.tlas_need4 + max_leaf_inst + 1 + S.blas_need4 + 2;
     if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
     if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27) || S.nodes4.size() >= (1u << 27))

@@ -51,6 +51,7 @@ struct HostScene {
   int tlas_depth = 0, blas_depth = 0;   // BVH2 levels
   int tlas_need4 = 0, blas_need4 = 0;   // BVH4 stack entries along the worst root-to-leaf path
   int max_leaf_inst = 0;                 // most instances in one world leaf (stack bound)
+  int quant_nodes = 0;                   // the traversal reads DNodeQ (RT_NODES_QUANT8, no RotateX/Z)
   // Mesh BLASes left to the device builder (RT_BLAS_DEVICE): their triangles
   // are in the arrays in reference DFS order; the BLAS header's root item is
   // a placeholder until build_mesh_blas (build.hip) fills it in.
@@ -73,6 +74,7 @@ struct FlattenOptions {
   int blas_builder = BLAS_SAH;
   int tlas_builder = BLAS_SAH;   // world BVH: SAH over the top-level objects, one per leaf
   int sah_min_prims = 16;   // smaller all-triangle BLASes keep the reference topology
+  int quant_nodes = 0;      // RT_NODES_QUANT8: the traversal reads DNodeQ (node_quant.h)
 };
 
 // (Re)builds S.inst_entries from refs / instances / blas headers: call after

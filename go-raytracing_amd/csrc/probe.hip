@@ -38,7 +38,7 @@ __global__ void tonemap_kernel(const float* accum, int n, int spp, uint8_t* rgba
 }
 
 // Parity probe: first-bounce closest hit of one sample per pixel.
-template <int STACK>
+template <int STACK, bool kQuant>
 __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, uint32_t seed, int sample,
                                                       int32_t* out_top, int32_t* out_prim, float* out_t, int* err) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack + world ray
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, ui
   get_ray(cam, px, py, key, ro, rd, time);
   Best b{};
   Cnt cnt = {};
-  bool hit = traverse<false, false>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack_only(lds_stack + tid, 256, STACK), b, key,
+  bool hit = traverse<false, false, true, kQuant>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack_only(lds_stack + tid, 256, STACK), b, key,
                                     0, DOM_VOL, cnt, err);
   int top = -1, prim = -1;
   if (hit) {
@@ -83,10 +83,14 @@ hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, i
                           int32_t* prim, float* t, int* err, int stack, hipStream_t st) {
   int n = cam.width * cam.height;
   dim3 grid((n + 255) / 256), block(256);
-  if (stack <= 32)
-    hipLaunchKernelGGL((primary_kernel<32>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
-  else
-    hipLaunchKernelGGL((primary_kernel<64>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+  const bool q = sc.quant_nodes != 0;   // the node format the renders traverse
+  if (stack <= 32) {
+    if (q) hipLaunchKernelGGL((primary_kernel<32, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+    else hipLaunchKernelGGL((primary_kernel<32, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+  } else {
+    if (q) hipLaunchKernelGGL((primary_kernel<64, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+    else hipLaunchKernelGGL((primary_kernel<64, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+  }
   return hipGetLastError();
 }
 

@@ -178,7 +178,7 @@ __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_
 // that finishes starts its next ray on the following step without waiting.
 // kFirst: bounce 0, the rays are the camera rays of the claimed slots (the
 // prefetch loads only the slot's pixel; GetRay runs when the ray starts).
-template <int STACK, bool kCount, bool kVol, bool kFirst>
+template <int STACK, bool kCount, bool kVol, bool kFirst, bool kQuant = false>
 __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_extend(DScene sc, DCamera cam, WaveArgs a,
                                                                 PathStream cs, const uint32_t* count,
                                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<false, kCount, kVol>(sc, T, S, cnt, a.err);
+      const int s = trav_step<false, kCount, kVol, kQuant>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
   }
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
 // the job's visibility bits go to sj_vis (k_nee_apply sums the visible
 // contributions in that order, camera.go:549-558).  Lanes prefetch their next
 // job as k_extend does.
-template <int STACK, bool kCount, bool kVol, bool kEnvIS>
+template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kQuant = false>
 __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<true, kCount, kVol>(sc, T, S, cnt, a.err);
+      const int s = trav_step<true, kCount, kVol, kQuant>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
   }
@@ -688,7 +688,7 @@ static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
   return hipEventRecord(plan.events[n++], st);
 }
 
-template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy>
+template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
   const int cus = plan.num_cus;
   hipError_t e;
@@ -704,7 +704,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
     if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
     const int max_trav_blocks = int(a.spill_lanes / 256u);   // one spill column per resident lane
     const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, 0, nslots, cus);
-    int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS>, 256, 0, nslots, cus);
+    int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus);
     gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;
     const int gap = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
     for (int b = 0; b < plan.max_depth; ++b) {
@@ -716,26 +716,26 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
       if ((e = mark(plan, KC_EXTEND, st)) != hipSuccess) return e;
       // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
       if (b == 0) {
-        const void* fx = (const void*)k_extend<STACK, kCount, kVol, true>;
+        const void* fx = (const void*)k_extend<STACK, kCount, kVol, true, kQuant>;
         int gext = grid_for(fx, 256, 0, nslots, cus);
         gext = gext < max_trav_blocks ? gext : max_trav_blocks;
-        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
+        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
       } else {
-        const void* fx = (const void*)k_extend<STACK, kCount, kVol, false>;
+        const void* fx = (const void*)k_extend<STACK, kCount, kVol, false, kQuant>;
         int gext = grid_for(fx, 256, 0, nslots, cus);
         gext = gext < max_trav_blocks ? gext : max_trav_blocks;
-        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
+        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
       }
       if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS>), dim3(gsd), dim3(256), 0, st, sc, a, cnt_shadow,
+      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd), dim3(256), 0, st, sc, a, cnt_shadow,
                          fetch_sh, fetch_ext);
       if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
       hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap), dim3(256), 0, st, a, cnt_shadow);
@@ -763,17 +763,24 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
   if (plan.max_depth > 0) {
     // the kVol variants also carry the rare primitives (circles)
     const bool vol = sc.has_volumes != 0 || sc.n_circles > 0;
-#define RUN(S, C, V)                                                              \
-  do {                                                                            \
-    if (envis) {                                                                  \
-      if (fancy) e = run_batches<S, C, V, true, true>(sc, cam, a, plan, st);      \
-      else e = run_batches<S, C, V, true, false>(sc, cam, a, plan, st);           \
-    } else {                                                                      \
-      if (fancy) e = run_batches<S, C, V, false, true>(sc, cam, a, plan, st);     \
-      else e = run_batches<S, C, V, false, false>(sc, cam, a, plan, st);          \
-    }                                                                             \
+#define RUN2(S, C, V, Q)                                                           \
+  do {                                                                             \
+    if (envis) {                                                                   \
+      if (fancy) e = run_batches<S, C, V, true, true, Q>(sc, cam, a, plan, st);    \
+      else e = run_batches<S, C, V, true, false, Q>(sc, cam, a, plan, st);         \
+    } else {                                                                       \
+      if (fancy) e = run_batches<S, C, V, false, true, Q>(sc, cam, a, plan, st);   \
+      else e = run_batches<S, C, V, false, false, Q>(sc, cam, a, plan, st);        \
+    }                                                                              \
   } while (0)
-    const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0;
+    // RT_NODES_QUANT8 scenes run the quantised-node traversal (its own kernels:
+    // the default fp32 kernels carry no trace of it)
+#define RUN(S, C, V)                            \
+  do {                                          \
+    if (quant) RUN2(S, C, V, true);             \
+    else RUN2(S, C, V, false);                  \
+  } while (0)
+    const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0, quant = sc.quant_nodes != 0;
 #ifdef RTG_RING24
     // diagnostic build only: the 24-entry ring of the round-1 fault
     if (stack > 16) {
@@ -789,6 +796,7 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
       else { if (count) RUN(8, true, false); else RUN(8, false, false); }
     }
 #undef RUN
+#undef RUN2
     if (e != hipSuccess) return e;
   }
   if (!count)

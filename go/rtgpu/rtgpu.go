@@ -88,9 +88,12 @@ const (
 const (
 	OptBLASBuilder int32 = 1 // RT_OPT_BLAS_BUILDER
 	OptTLASBuilder int32 = 2 // RT_OPT_TLAS_BUILDER
+	OptNodeFormat  int32 = 3 // RT_OPT_NODE_FORMAT
 	BuildReference int32 = 0 // RT_BLAS_REFERENCE
 	BuildSAH       int32 = 1 // RT_BLAS_SAH
 	BuildDevice    int32 = 2 // RT_BLAS_DEVICE
+	NodesFP32      int32 = 0 // RT_NODES_FP32
+	NodesQuant8    int32 = 1 // RT_NODES_QUANT8
 )
 
 // Node mirrors rt_hittable: one node per concrete rt.Hittable.  P holds the

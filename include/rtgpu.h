@@ -258,9 +258,18 @@ const char* rt_last_error(const rt_ctx* ctx);
  *     RT_BLAS_REFERENCE = the caller's topology; RT_BLAS_SAH (default) =
  *     SAH over the same top-level objects, one per leaf, each keeping its
  *     DFS rank and its leaf's test count (volumes).  Scenes holding a
- *     RotateX/RotateZ wrapper always keep the caller's topology.          */
-enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2 };
+ *     RotateX/RotateZ wrapper always keep the caller's topology.
+ *   RT_OPT_NODE_FORMAT: the BVH4 node records the traversal reads:
+ *     RT_NODES_FP32 (default) = 128-B nodes, fp32 child boxes rounded
+ *     outward from the fp64 boxes; RT_NODES_QUANT8 = 64-B nodes, child
+ *     planes as 8-bit steps of a per-node frame, widened by a margin that
+ *     covers the slab test's rounding (half the node bytes, looser boxes;
+ *     the same closest hits).  Scenes holding a RotateX/RotateZ wrapper
+ *     always use RT_NODES_FP32 (their node boxes decide which rays reach
+ *     an object, transform.go:201-351).                                   */
+enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
+enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);
 
 /* Flatten + upload the Go object graph (copied; caller memory not retained). */

@@ -11,6 +11,7 @@
 
 #include "../go-raytracing_amd/csrc/dev_layout.h"
 #include "../go-raytracing_amd/csrc/flatten.h"
+#include "../go-raytracing_amd/csrc/node_quant.h"
 #include "../include/rtscene.h"
 
 namespace emu {
@@ -26,6 +27,7 @@ struct EmuScene {
   // the device buffers have (api.cpp upload_vec)
   std::vector<std::vector<char>> padded;
   HostScene h;
+  std::vector<DNodeQ> qnodes;   // quantised nodes (build.hip k_quantize, same function)
   DScene d{};
   DCamera cam{};
   int max_depth = 0;
@@ -42,7 +44,9 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   char err[512] = {0};
   if (rts_scene_create(name, &opt, &E.scn, err, sizeof err) != 0) { fprintf(stderr, "%s\n", err); return 3; }
   std::string ferr;
-  if (flatten_scene(rts_scene_get_desc(E.scn), E.h, ferr)) { fprintf(stderr, "%s\n", ferr.c_str()); return 4; }
+  FlattenOptions fo;
+  if (const char* nf = getenv("RTG_EMU_QUANT")) fo.quant_nodes = atoi(nf);   // node format under test
+  if (flatten_scene(rts_scene_get_desc(E.scn), E.h, ferr, fo)) { fprintf(stderr, "%s\n", ferr.c_str()); return 4; }
   const HostScene& h = E.h;
   DScene& d = E.d;
   auto pad = [&](const auto& v) {
@@ -59,6 +63,11 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.circle_hidx = ptr(h.circle_hidx); d.perlins = ptr(h.perlins); d.images = ptr(h.images);
   d.image_texels = ptr(h.image_texels); d.planes = ptr(h.planes); d.instances = ptr(h.instances); d.blas = ptr(h.blas);
   d.inst_entry = ptr(h.inst_entries);
+  if (h.quant_nodes) {
+    E.qnodes.resize(h.nodes4.size());
+    for (size_t i = 0; i < h.nodes4.size(); ++i) E.qnodes[i] = quantize_node(h.nodes4[i]);
+    d.qnodes = pad(E.qnodes);
+  }
   d.leaves = pad(h.leaves); d.tris = pad(h.tris); d.quads = pad(h.quads); d.spheres = pad(h.spheres);
   d.quad_wref = ptr(h.quad_wref); d.sphere_wref = ptr(h.sphere_wref);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
@@ -74,6 +83,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.num_planes = int(h.planes.size()); d.num_lights = int(h.lights.size());
   d.num_materials = int(h.materials.size()); d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed; d.has_volumes = h.volumes.empty() ? 0 : 1;
+  d.quant_nodes = h.quant_nodes;
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());

@@ -17,6 +17,7 @@
 #define RTG_HOST_EMU 1
 struct float4 { float x, y, z, w; };
 struct uint4 { uint32_t x, y, z, w; };
+struct uint2 { uint32_t x, y; };
 struct int4 { int x, y, z, w; };
 inline float4 make_float4(float x, float y, float z, float w) { return float4{x, y, z, w}; }
 // Wave vote with random wave-mates: returns p, or true at random when p is

@@ -90,3 +90,42 @@ def test_wavefront_kernels_under_asan_match_oracle(wave, O, g, tmp_path, name, b
     ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
     got = np.fromfile(out, np.float32).reshape(ref.shape)
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())
+
+
+def test_node_quantiser_is_conservative(tmp_path):
+    """RT_NODES_QUANT8 (node_quant.h): on random BVH4 nodes spanning ten
+    decades, every child's dequantised box holds its fp32 box with the stated
+    margin, unused children are rejected, and the traversal's fp32 quantised
+    slab test accepts rays aimed at faces, edges and corners from up to 20
+    node magnitudes away (tests/quant_probe.cpp)."""
+    exe = tmp_path / "qp"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "tests", "host_emu"),
+                    os.path.join(ROOT, "tests", "quant_probe.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "20000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    info = json.loads(r.stdout)
+    assert info["rays"] == 160000 and info["contain_fail"] == info["unused_fail"] == info["slab_fail"] == 0, info
+
+
+@pytest.mark.parametrize("name,batch", [("cornell-lucy", 1), ("random", 0), ("cornell-smoke", 0), ("hdri-nee", 0),
+                                        ("primitives", 1), ("cornell-rotations", 0)])
+def test_wavefront_kernels_quant8_nodes_match_oracle(wave, O, g, tmp_path, name, batch):
+    """The same host emulation with the quantised node format
+    (RT_NODES_QUANT8; cornell-rotations keeps fp32 nodes): same oracle bar."""
+    spp, seed, width = 2, 77, 40
+    out = tmp_path / f"{name}.f32"
+    args = [wave, name, str(width), str(spp), str(seed), ASSETS, str(out)]
+    if batch:
+        args.append(str(batch))
+    env = _env()
+    env["RTG_EMU_QUANT"] = "1"
+    r = subprocess.run(args, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    kw = dict(width=width)
+    if name == "cornell-lucy":
+        kw.update(lucy_rings=60, lucy_cols=80)
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
+    got = np.fromfile(out, np.float32).reshape(ref.shape)
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())

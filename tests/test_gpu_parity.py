@@ -93,6 +93,32 @@ def test_radiance_parity_fp32(g, O, ctx, name, kw):
     assert gpu.mean() > 0
 
 
+@pytest.mark.parametrize("name,kw", SCENES, ids=[s[0] for s in SCENES])
+def test_quant8_nodes_parity(g, O, name, kw):
+    """RT_NODES_QUANT8 (64-B quantised nodes, node_quant.h): first hits
+    bit-exact against the oracle (the boxes only cull) and the same radiance
+    bar as the fp32 nodes; cornell-rotations keeps its fp32 nodes."""
+    s = _scene(g, name, kw)
+    cam = s.camera
+    c = g.Context(0)
+    try:
+        c.set_node_format("quant8")
+        c.upload(s.desc)
+        tg, pg, t_g = c.primary_hits(cam, 1234, 3)
+        to, po, t_o = O.primary_hits(s.desc, cam, 1234, 3, fp32=True)
+        assert np.array_equal(tg, to) and np.array_equal(pg, po), f"{name}: hit ids differ"
+        hit = tg >= 0
+        assert np.array_equal(t_g[hit], t_o[hit].astype(np.float32)), f"{name}: hit t differs"
+        spp = 8
+        p = g.make_params(spp, cam.max_depth, seed=77)
+        gpu, _ = c.render(cam, p)
+        ref = O.render(s.desc, cam, p, fp32=True)
+        mse = float(np.mean((gpu.astype(np.float64) / spp - ref / spp) ** 2))
+        assert np.isfinite(gpu).all() and mse < 1e-4, f"{name}: mse {mse:.3e}"
+    finally:
+        c.close()
+
+
 # BASELINE configs (C1 SimpleScene, C2 RandomScene, C3 CornellBoxScene, C4
 # CornellBoxLucy with the full 280K-triangle mesh, C5 HDRITestScene) at reduced
 # resolution, plus the fog and RotateX/Z variants: (scene, kwargs, spp).  The

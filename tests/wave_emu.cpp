@@ -24,7 +24,7 @@ namespace {
 
 constexpr int kRing = 4;
 
-template <bool kVol, bool kEnvIS, bool kFancy>
+template <bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
 void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_t spb, int max_depth, float* out) {
   uint32_t* cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
   uint32_t* cnt_shadow = a.counts + CNT_SHADOW;
@@ -38,15 +38,15 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
     for (int b = 0; b < max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
       if (b == 0) {
-        k_extend<kRing, false, kVol, true>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
+        k_extend<kRing, false, kVol, true, kQuant>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
                                            fetch_ext, s0);
         k_shade<false, kEnvIS, kFancy, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       } else {
-        k_extend<kRing, false, kVol, false>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
+        k_extend<kRing, false, kVol, false, kQuant>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
                                             fetch_ext, s0);
         k_shade<false, kEnvIS, kFancy, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       }
-      k_shadow<kRing, false, kVol, kEnvIS>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
+      k_shadow<kRing, false, kVol, kEnvIS, kQuant>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
       k_nee_apply<kEnvIS>(a, cnt_shadow);
     }
     k_accum(a, sb);
@@ -106,7 +106,11 @@ int main(int argc, char** argv) {
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
   const bool vol = d.has_volumes != 0 || d.n_circles > 0, envis = d.env.valid && d.env.use_is, fancy = d.has_fancy != 0;
-#define RUN(V, H, F) run<V, H, F>(d, cam, a, spp, spb, E.max_depth, out.data())
+#define RUN(V, H, F)                                                  \
+  do {                                                                \
+    if (d.quant_nodes) run<V, H, F, true>(d, cam, a, spp, spb, E.max_depth, out.data()); \
+    else run<V, H, F, false>(d, cam, a, spp, spb, E.max_depth, out.data()); \
+  } while (0)
   if (vol) {
     if (envis) { if (fancy) RUN(true, true, true); else RUN(true, true, false); }
     else { if (fancy) RUN(true, false, true); else RUN(true, false, false); }
