@@ -295,6 +295,9 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
   }
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
+  // without lights no k_shadow runs (run_batches): reset the next extend's
+  // fetch counter here (this extend has finished claiming)
+  if (sc.num_lights == 0 && blockIdx.x == 0 && threadIdx.x == 0) a.counts[CNT_FETCH_EXT] = 0u;
   Cnt cnt = {};
   // block-uniform trip count (blockDim 256, gs a multiple of 256): every
   // thread reaches the block_reserve2 barriers
@@ -691,6 +694,7 @@ static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
 template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
   const int cus = plan.num_cus;
+  const bool nee = sc.num_lights > 0;
   hipError_t e;
   uint32_t* const cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
   uint32_t* const cnt_shadow = a.counts + CNT_SHADOW;
@@ -734,11 +738,16 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
         hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
       }
-      if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd), dim3(256), 0, st, sc, a, cnt_shadow,
-                         fetch_sh, fetch_ext);
-      if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap), dim3(256), 0, st, a, cnt_shadow);
+      // no lights: k_shade writes no NEE job (sampleLightMIS needs a light,
+      // camera.go:502), so the shadow and apply launches are skipped; k_shade
+      // then resets the next extend's fetch counter itself
+      if (nee) {
+        if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd), dim3(256), 0, st, sc, a,
+                           cnt_shadow, fetch_sh, fetch_ext);
+        if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap), dim3(256), 0, st, a, cnt_shadow);
+      }
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
         // long-tail scenes (RandomScene depth 50): stop once every path ended
         uint32_t left = 0;

@@ -46,8 +46,10 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
                                             fetch_ext, s0);
         k_shade<false, kEnvIS, kFancy, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       }
-      k_shadow<kRing, false, kVol, kEnvIS, kQuant>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
-      k_nee_apply<kEnvIS>(a, cnt_shadow);
+      if (sc.num_lights > 0) {   // as run_batches: no lights, no NEE launches
+        k_shadow<kRing, false, kVol, kEnvIS, kQuant>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
+        k_nee_apply<kEnvIS>(a, cnt_shadow);
+      }
     }
     k_accum(a, sb);
   }
