@@ -1196,8 +1196,15 @@ __device__ V3 env_sample(const DEnv& e, V3 dir) {          // hdri.go:120-128 + 
   int x0 = int(floorf(px)), y0 = int(floorf(py));
   int x1 = x0 + 1, y1 = y0 + 1;
   float fx = px - float(x0), fy = py - float(y0);
-  x0 = ((x0 % e.width) + e.width) % e.width;
-  x1 = ((x1 % e.width) + e.width) % e.width;
+  // ((x % w) + w) % w without the integer divisions for the in-range case
+  // (u in [0, 1) puts x0 in [-1, w - 1] and x1 in [0, w]); the general form
+  // stays for anything else (a NaN direction)
+  auto wrapx = [&](int x) {
+    if (x >= -e.width && x < 2 * e.width) return x < 0 ? x + e.width : (x >= e.width ? x - e.width : x);
+    return ((x % e.width) + e.width) % e.width;
+  };
+  x0 = wrapx(x0);
+  x1 = wrapx(x1);
   y0 = iclamp(y0, 0, e.height);
   y1 = iclamp(y1, 0, e.height);
   V3 c00 = texel(e, x0, y0), c10 = texel(e, x1, y0), c01 = texel(e, x0, y1), c11 = texel(e, x1, y1);
