@@ -790,12 +790,17 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     else RUN2(S, C, V, false);                  \
   } while (0)
     const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0, quant = sc.quant_nodes != 0;
-#ifdef RTG_RING24
-    // diagnostic build only: the 24-entry ring of the round-1 fault,
-    // for every scene, fp32 nodes, no counting variant (a short compile)
+#if defined(RTG_RING24) && !defined(RTG_DIAG_RING)
+#define RTG_DIAG_RING 24
+#endif
+#ifdef RTG_DIAG_RING
+    // diagnostic builds only (RTG_GUARD / RTG_RING24 bisection):
+    // one ring size for every scene, fp32 nodes, no counting variant (a
+    // short compile)
     (void)quant;
+    (void)stack;
     if (count) return hipErrorNotSupported;
-    if (vol) RUN2(24, false, true, false); else RUN2(24, false, false, false);
+    if (vol) RUN2(RTG_DIAG_RING, false, true, false); else RUN2(RTG_DIAG_RING, false, false, false);
 #else
     if (stack > 8) {
       if (vol) { if (count) RUN(16, true, true); else RUN(16, false, true); }
