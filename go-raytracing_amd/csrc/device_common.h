@@ -420,6 +420,47 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
   // rec1: closest over the universe interval; rec2: closest over (t1+1e-4, inf).
   float t1 = __builtin_inff(), t2 = __builtin_inff();
   bool h1 = false, h2 = false;
+  constexpr int kCache = 6;   // a Box boundary: six quads
+  if (n <= kCache) {
+    // Only the two closest distances matter, and a quad's / triangle's hit
+    // distance does not depend on the interval's lower bound (quad_t / tri_t
+    // test it last): each is intersected once, with the bound -inf, and both
+    // passes filter the cached distances (the same values the two-pass loop
+    // below computes, so the same t1, t2).  Spheres pick their root by the
+    // bound and are intersected per pass.
+    float tq[kCache];
+    uint32_t valid = 0u, sph = 0u;
+    const float ninf = -__builtin_inff();
+    for (int k = 0; k < kCache; ++k) {
+      tq[k] = 0.0f;
+      if (k >= n) continue;
+      int pk = kind; uint32_t pi = lf.first + k;
+      if (kind == PK_MIXED) { uint32_t r = sc.refs[GIX(pi, sc.n_refs, 4)]; pk = int(r >> REF_SHIFT); pi = r & REF_MASK; }
+      bool ok = false;
+      if (pk == PK_QUAD) ok = quad_t(sc.quads[GIX(pi, sc.n_quads, 5)], o, d, ninf, tq[k]);
+      else if (pk == PK_TRI) ok = tri_t(sc.tris[GIX(pi, sc.n_tris, 6)], o, d, ninf, tq[k]);
+      else if (pk == PK_SPHERE) { sph |= 1u << k; tq[k] = __uint_as_float(pi); }
+      if (ok) valid |= 1u << k;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      const float lo = pass == 0 ? ninf : t1 + 0.0001f;
+      float closest = __builtin_inff();
+      bool found = false;
+      for (int k = 0; k < kCache; ++k) {
+        if ((valid >> k) & 1u) {
+          if (lo <= tq[k] && tq[k] <= closest) { closest = tq[k]; found = true; }
+        } else if ((sph >> k) & 1u) {
+          float t = 0.0f;
+          if (sphere_t(sc.spheres[GIX(__float_as_uint(tq[k]), sc.n_spheres, 7)], o, d, time, lo, t) && t < closest) {
+            closest = t;
+            found = true;
+          }
+        }
+      }
+      if (pass == 0) { h1 = found; t1 = closest; if (!h1) break; }
+      else { h2 = found; t2 = closest; }
+    }
+  } else
   for (int pass = 0; pass < 2; ++pass) {
     float lo = pass == 0 ? -__builtin_inff() : t1 + 0.0001f;
     float closest = __builtin_inff();
