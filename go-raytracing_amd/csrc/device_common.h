@@ -635,6 +635,24 @@ __device__ __forceinline__ void resolve_inst(const DScene& sc, Best& b) {
 
 enum : int { TRAV_RUNNING = 0, TRAV_DONE = 1, TRAV_ANYHIT = 2 };
 
+// Phase 1 of a while-while round ends once at most this many lanes of the
+// wave still lack a postponed leaf / instance item (0 = every lane holds one,
+// Aila & Laine's rule).  The last few lanes' node walks otherwise hold the
+// whole wave in phase 1 while the others wait.
+#ifndef RTG_P1_SLACK
+#define RTG_P1_SLACK 16
+#endif
+#ifndef RTG_P1_SLACK_ANY
+#define RTG_P1_SLACK_ANY RTG_P1_SLACK
+#endif
+// The rare-primitive (fog) variants measured best at 0: CornellBoxScene 985
+// vs 956 Msamples/s at 16; CornellBoxLucy 1445 at 0, 1662 at 4, 1770 at 16,
+// 1756 at 24, 1720 at 32, 1507 at 48.
+#ifndef RTG_P1_SLACK_VOL
+#define RTG_P1_SLACK_VOL 0
+#endif
+constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackVol = RTG_P1_SLACK_VOL;
+
 // accept() on the split record: a hit was accepted iff bt < tmax (the first
 // acceptance needs t < tmax), and the tie rule reads the LDS words.
 __device__ __forceinline__ bool accept_hit(const DScene& sc, float t, int kind, int refpos, int primpos, const Trav& T,
@@ -831,7 +849,8 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       cnt.st_load += st1 - st0; cnt.st_math += st2 - st1; cnt.st_rest += st3 - st2; cnt.st_steps++;
     }
 #endif
-    if (!__any(T.lf == ITEM_NONE)) break;   // every lane holds a postponed item
+    // leave phase 1 once at most kP1Slack lanes lack a postponed item
+    if (__popcll(__ballot(T.lf == ITEM_NONE)) <= (kVol ? kP1SlackVol : kAny ? kP1SlackAny : kP1Slack)) break;
   }
   // ---------------- phase 2: leaves, instance entry / exit
 #ifdef RTG_STAMP
