@@ -652,6 +652,10 @@ enum : int { TRAV_RUNNING = 0, TRAV_DONE = 1, TRAV_ANYHIT = 2 };
 #define RTG_P1_SLACK_VOL 0
 #endif
 constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackVol = RTG_P1_SLACK_VOL;
+#ifndef RTG_P2_SLACK
+#define RTG_P2_SLACK 0
+#endif
+constexpr int kP2Slack = RTG_P2_SLACK;
 
 // accept() on the split record: a hit was accepted iff bt < tmax (the first
 // acceptance needs t < tmax), and the tie rule reads the LDS words.
@@ -1043,6 +1047,9 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       cnt.st_tail += se - sb; cnt.st_rounds++;
     }
 #endif
+    // leave phase 2 once at most kP2Slack lanes would process another item
+    // (they keep it postponed for the next round)
+    if (kP2Slack > 0 && __popcll(__ballot(T.lf != ITEM_NONE)) <= kP2Slack) break;
   }
 #ifdef RTG_STAMP
   if (st_lead2) cnt.st_p2 += rtg_stamp() - st4;
