@@ -29,6 +29,7 @@ ASSET_DIR = os.path.join(REPO_DIR, "assets")
 
 RT_OK = 0
 RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER, RT_OPT_NODE_FORMAT = 1, 2, 3
+RT_OPT_BATCH_SLOTS, RT_OPT_REFILL, RT_OPT_MAX_BLOCKS = 4, 5, 6
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
@@ -155,6 +156,11 @@ def rtgpu() -> C.CDLL:
         P, I32, U32 = C.c_void_p, C.c_int32, C.c_uint32
         lib.rt_abi_version.restype = C.c_int
         lib.rt_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
+        # (A/B builds of older revisions, RTGPU_LIB_DIR, may lack the newer entry points)
+        if hasattr(lib, "rt_ctx_create_multi"):
+            lib.rt_ctx_create_multi.argtypes = [C.POINTER(I32), I32, C.POINTER(P)]
+            lib.rt_ctx_num_devices.argtypes = [P]
+            lib.rt_device_count.argtypes = [C.POINTER(I32)]
         lib.rt_ctx_destroy.argtypes = [P]
         lib.rt_ctx_destroy.restype = None
         lib.rt_last_error.argtypes = [P]
@@ -177,6 +183,9 @@ def rtgpu() -> C.CDLL:
         lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
         lib.rt_primary_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32), C.POINTER(I32),
                                         C.POINTER(C.c_float)]
+        if hasattr(lib, "rt_extend_first_hits"):
+            lib.rt_extend_first_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32),
+                                                 C.POINTER(I32), C.POINTER(C.c_float)]
         _rtgpu = lib
     return _rtgpu
 
@@ -212,6 +221,8 @@ def rtscene() -> C.CDLL:
         lib.rts_renderer_save_png.argtypes = [P, C.c_char_p]
         lib.rts_renderer_last_error.argtypes = [P]
         lib.rts_renderer_last_error.restype = C.c_char_p
+        if hasattr(lib, "rts_renderer_timings"):
+            lib.rts_renderer_timings.argtypes = [P, C.POINTER(C.c_double)]
         lib.rts_load_hdr.argtypes = [C.c_char_p, C.POINTER(I32), C.POINTER(I32), C.POINTER(C.c_double), C.c_int64]
         lib.rts_write_synthetic_lucy_obj.argtypes = [C.c_char_p, I32, I32]
         lib.rts_obj_triangle_count.argtypes = [C.c_char_p]
@@ -349,17 +360,39 @@ def make_params(spp: int, depth: int, seed: int = 1, sample_offset: int = 0, buc
 # ---------------------------------------------------------------------------
 # GPU context (rt_ctx)
 # ---------------------------------------------------------------------------
-class Context:
-    """One device's flattened scene + render entry points (rtgpu.h)."""
+def device_count() -> int:
+    """Visible HIP devices (rt_device_count)."""
+    n = C.c_int32()
+    rc = rtgpu().rt_device_count(C.byref(n))
+    if rc != RT_OK:
+        raise RTError(rc, "rt_device_count failed (no GPU?)")
+    return n.value
 
-    def __init__(self, device: int = 0):
+
+class Context:
+    """One device's flattened scene + render entry points (rtgpu.h).  With
+    `devices=[d0, d1, ...]` one context over several devices
+    (rt_ctx_create_multi): renders deal the buckets round-robin over them."""
+
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
         self._lib = rtgpu()
         h = C.c_void_p()
-        rc = self._lib.rt_ctx_create(device, C.byref(h))
-        if rc != RT_OK:
-            raise RTError(rc, f"rt_ctx_create(device={device}) failed (no GPU?)")
+        if devices is not None and len(devices) > 0:
+            arr = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            rc = self._lib.rt_ctx_create_multi(arr, len(devices), C.byref(h))
+            if rc != RT_OK:
+                raise RTError(rc, f"rt_ctx_create_multi(devices={list(devices)}) failed")
+            device = int(devices[0])
+        else:
+            rc = self._lib.rt_ctx_create(device, C.byref(h))
+            if rc != RT_OK:
+                raise RTError(rc, f"rt_ctx_create(device={device}) failed (no GPU?)")
         self._h = h
         self.device = device
+
+    @property
+    def num_devices(self) -> int:
+        return int(self._lib.rt_ctx_num_devices(self._h))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -437,6 +470,14 @@ class Context:
         8-bit child planes with a conservative margin); next upload."""
         self.set_option(RT_OPT_NODE_FORMAT, {"fp32": RT_NODES_FP32, "quant8": RT_NODES_QUANT8}[fmt])
 
+    def set_schedule(self, batch_slots: int = 0, refill: int = 0, max_blocks: int = 0):
+        """Schedule options (0 = automatic) for the next renders: path slots per
+        batch, idle lanes before a wave claims more rays, cap on the persistent
+        traversal grids.  They never change the image."""
+        self.set_option(RT_OPT_BATCH_SLOTS, batch_slots)
+        self.set_option(RT_OPT_REFILL, refill)
+        self.set_option(RT_OPT_MAX_BLOCKS, max_blocks)
+
     def set_kernel_timing(self, enable: bool = True):
         self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))
 
@@ -460,6 +501,16 @@ class Context:
         t = np.zeros(n, np.float32)
         self._check(self._lib.rt_primary_hits(self._h, C.byref(camera), seed, sample, _i32p(top), _i32p(prim),
                                               _f32p(t)))
+        return top, prim, t
+
+    def extend_first_hits(self, camera: RtCameraDesc, seed: int, sample: int = 0):
+        """primary_hits' ids from the production pipeline's first k_extend."""
+        n = camera.image_width * camera.image_height
+        top = np.zeros(n, np.int32)
+        prim = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        self._check(self._lib.rt_extend_first_hits(self._h, C.byref(camera), seed, sample, _i32p(top), _i32p(prim),
+                                                   _f32p(t)))
         return top, prim, t
 
 
@@ -509,6 +560,13 @@ class BucketRenderer:
 
     def duration_ms(self) -> float:
         return float(self._lib.rts_renderer_duration_ms(self._h))
+
+    def timings(self) -> dict:
+        """Construction ms (context + scene upload), each pass's wall ms (host
+        buffers + tonemap) and its device render ms."""
+        t = (C.c_double * 7)()
+        self._check(self._lib.rts_renderer_timings(self._h, t))
+        return {"create_ms": t[0], "pass_wall_ms": [t[1], t[2], t[3]], "pass_render_ms": [t[4], t[5], t[6]]}
 
     def save_image(self, path: str):
         self._check(self._lib.rts_renderer_save_png(self._h, path.encode()))

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rtgpu.h"
@@ -62,9 +63,21 @@ struct rt_ctx {
   std::vector<uint8_t> tev_class;
   int tev_used = 0;
   FlattenOptions fopt;
+  // schedule options (RT_OPT_BATCH_SLOTS / RT_OPT_REFILL / RT_OPT_MAX_BLOCKS;
+  // 0 = automatic): they change how the work is dealt, never the result
+  size_t opt_slots = 0;
+  int opt_refill = 0;
+  int opt_blocks = 0;
   // device BVH build (RT_BLAS_DEVICE) of the last upload
   uint32_t dev_nodes = 0, dev_leaves = 0;   // nodes / leaves added on the device
   double build_ms = 0.0;                    // wall time of the device builds
+  // multi-device context (rt_ctx_create_multi): this context is devices[0]
+  // and owns one sub-context per further device; a render deals the buckets
+  // round-robin over all of them (bucket_renderer.go:193-213's worker pool,
+  // one GPU per worker)
+  std::vector<rt_ctx*> subs;
+  hipEvent_t fan_ev = nullptr;    // caller-stream point the devices' renders start after
+  hipEvent_t join_ev = nullptr;   // end of this device's share of a render
 };
 
 namespace {
@@ -246,7 +259,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     const char* e = getenv("RTGPU_SLOTS");
     return e && atol(e) > 0 ? size_t(atol(e)) : size_t(0);
   }();
-  size_t target = env_slots;
+  size_t target = ctx->opt_slots ? ctx->opt_slots : env_slots;
   if (!target) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = size_t(8) << 30;
@@ -313,8 +326,9 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     const char* e = getenv("RTGPU_REFILL");
     return e ? std::min(64, std::max(1, atoi(e))) : 16;
   }();
-  a.refill = refill;
+  a.refill = ctx->opt_refill ? ctx->opt_refill : refill;
   WavePlan plan{};
+  plan.max_blocks = ctx->opt_blocks;
   plan.spp = spp;
   plan.samples_per_batch = spb;
   plan.sample_offset = uint32_t(p->sample_offset);
@@ -411,6 +425,71 @@ int render_impl(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* 
   return render_wave(ctx, dc, p, tiles, d_out, st, count, host_counters, ms);
 }
 
+// ---- multi-device contexts (rt_ctx_create_multi)
+// Runs f(k, ctx_k) for the context and each sub-context, one host thread per
+// device (each sets its device first); the first failure's status is
+// returned with its message on `ctx`.
+template <class F>
+int fan_out(rt_ctx* ctx, F f) {
+  if (ctx->subs.empty()) return f(0, ctx);
+  std::vector<rt_ctx*> cs{ctx};
+  cs.insert(cs.end(), ctx->subs.begin(), ctx->subs.end());
+  std::vector<int> rc(cs.size(), RT_OK);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < cs.size(); ++k)
+    th.emplace_back([&, k] {
+      if (hipSetDevice(cs[k]->device) != hipSuccess) { rc[k] = set_err(cs[k], RT_ERR_HIP, "hipSetDevice"); return; }
+      rc[k] = f(int(k), cs[k]);
+    });
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < cs.size(); ++k)
+    if (rc[k]) {
+      if (k) ctx->error = "device " + std::to_string(cs[k]->device) + ": " + cs[k]->error;
+      return rc[k];
+    }
+  return RT_OK;
+}
+
+// One device's share of a multi-device render: its buckets into the
+// caller's frame on devices[0], on its own stream after the caller's stream
+// has reached fan_ev.
+int render_share(rt_ctx* ctx, rt_ctx* primary, const rt_camera_desc* cam, const rt_render_params* p,
+                 const std::vector<rt_bucket>& share, float* d_out, hipStream_t caller) {
+  ctx->kev_recorded = false;
+  if (share.empty()) return RT_OK;
+  rt_render_params q = *p;
+  q.buckets = share.data();
+  q.num_buckets = int32_t(share.size());
+  const bool first = ctx == primary;
+  hipStream_t s = first ? caller : ctx->stream;
+  if (!first) HIPCHK(hipStreamWaitEvent(s, primary->fan_ev, 0));
+  int rc = render_impl(ctx, cam, &q, d_out, s, false, nullptr, nullptr);
+  if (rc) return rc;
+  if (!first) HIPCHK(hipEventRecord(ctx->join_ev, s));
+  return RT_OK;
+}
+
+// Deals the buckets round-robin over the devices (tile k to
+// device k mod G balances the centre-heavy cost of the centre-out bucket
+// order) and renders every share concurrently; the caller's stream waits for
+// all of them.  Each pixel has one owner, so the frame equals one device's.
+int render_multi(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* p, float* d_out, hipStream_t st) {
+  if (!p || !cam) return set_err(ctx, RT_ERR_INVALID, "camera / params is NULL");
+  if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
+  std::vector<rt_bucket> bk;
+  if (p->buckets && p->num_buckets > 0) bk.assign(p->buckets, p->buckets + p->num_buckets);
+  else if (p->buckets == nullptr) bk = default_buckets(cam->image_width, cam->image_height, 32);
+  const size_t n = 1 + ctx->subs.size();
+  std::vector<std::vector<rt_bucket>> share(n);
+  for (size_t i = 0; i < bk.size(); ++i) share[i % n].push_back(bk[i]);
+  HIPCHK(hipEventRecord(ctx->fan_ev, st));
+  int rc = fan_out(ctx, [&](int k, rt_ctx* c) -> int { return render_share(c, ctx, cam, p, share[size_t(k)], d_out, st); });
+  if (rc) return rc;
+  for (size_t k = 1; k < n; ++k)
+    if (!share[k].empty()) HIPCHK(hipStreamWaitEvent(st, ctx->subs[k - 1]->join_ev, 0));
+  return RT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -435,6 +514,8 @@ int rt_ctx_create(int device, rt_ctx** out) {
       hipEventCreate(&ctx->kev0) != hipSuccess || hipEventCreate(&ctx->kev1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->pix_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&ctx->probe_pinned), 64) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->fan_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess ||
       hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
     delete ctx;
     return RT_ERR_HIP;
@@ -443,8 +524,50 @@ int rt_ctx_create(int device, rt_ctx** out) {
   return RT_OK;
 }
 
+int rt_device_count(int32_t* n) {
+  if (!n) return RT_ERR_INVALID;
+  *n = 0;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return RT_ERR_HIP;
+  *n = c;
+  return RT_OK;
+}
+
+int rt_ctx_create_multi(const int32_t* devices, int32_t num_devices, rt_ctx** out) {
+  if (!out) return RT_ERR_INVALID;
+  *out = nullptr;
+  if (!devices || num_devices <= 0) return RT_ERR_INVALID;
+  rt_ctx* ctx = nullptr;
+  int rc = rt_ctx_create(devices[0], &ctx);
+  if (rc) return rc;
+  for (int k = 1; k < num_devices; ++k) {
+    rt_ctx* sub = nullptr;
+    if ((rc = rt_ctx_create(devices[k], &sub))) { rt_ctx_destroy(ctx); return rc; }
+    ctx->subs.push_back(sub);
+    if (devices[k] != devices[0]) {
+      // each device's k_finalize writes its pixels straight into the
+      // caller's frame on devices[0] (xGMI peer writes, no staging copy)
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[k], devices[0]) != hipSuccess || !can) {
+        rt_ctx_destroy(ctx);
+        return RT_ERR_UNSUPPORTED;
+      }
+      (void)hipSetDevice(devices[k]);
+      const hipError_t e = hipDeviceEnablePeerAccess(devices[0], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { rt_ctx_destroy(ctx); return RT_ERR_HIP; }
+      (void)hipGetLastError();   // clear a sticky "already enabled"
+    }
+  }
+  *out = ctx;
+  return RT_OK;
+}
+
+int rt_ctx_num_devices(const rt_ctx* ctx) { return ctx ? 1 + int(ctx->subs.size()) : 0; }
+
 void rt_ctx_destroy(rt_ctx* ctx) {
   if (!ctx) return;
+  for (rt_ctx* s : ctx->subs) rt_ctx_destroy(s);
+  ctx->subs.clear();
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   free_scene(ctx);
@@ -462,6 +585,8 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   (void)hipEventDestroy(ctx->kev1);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
+  if (ctx->fan_ev) (void)hipEventDestroy(ctx->fan_ev);
+  if (ctx->join_ev) (void)hipEventDestroy(ctx->join_ev);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -470,6 +595,10 @@ const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->error.c_str() :
 
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (!ctx) return RT_ERR_INVALID;
+  for (rt_ctx* s : ctx->subs) {   // multi-device: every device's context
+    const int rc = rt_ctx_set_option(s, key, value);
+    if (rc) return set_err(ctx, rc, s->error);
+  }
   if (key == RT_OPT_BLAS_BUILDER) {
     if (value != RT_BLAS_REFERENCE && value != RT_BLAS_SAH && value != RT_BLAS_DEVICE)
       return set_err(ctx, RT_ERR_INVALID, "bad BLAS builder");
@@ -484,6 +613,21 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (key == RT_OPT_NODE_FORMAT) {
     if (value != RT_NODES_FP32 && value != RT_NODES_QUANT8) return set_err(ctx, RT_ERR_INVALID, "bad node format");
     ctx->fopt.quant_nodes = value == RT_NODES_QUANT8 ? 1 : 0;
+    return RT_OK;
+  }
+  if (key == RT_OPT_BATCH_SLOTS) {
+    if (value < 0) return set_err(ctx, RT_ERR_INVALID, "bad batch slots");
+    ctx->opt_slots = size_t(value);
+    return RT_OK;
+  }
+  if (key == RT_OPT_REFILL) {
+    if (value < 0 || value > 64) return set_err(ctx, RT_ERR_INVALID, "refill must be 0 (default) or 1..64");
+    ctx->opt_refill = value;
+    return RT_OK;
+  }
+  if (key == RT_OPT_MAX_BLOCKS) {
+    if (value < 0) return set_err(ctx, RT_ERR_INVALID, "bad max blocks");
+    ctx->opt_blocks = value;
     return RT_OK;
   }
   return set_err(ctx, RT_ERR_INVALID, "unknown option " + std::to_string(key));
@@ -539,8 +683,15 @@ static int device_builds(rt_ctx* ctx) {
   return RT_OK;
 }
 
+static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene);
+
 int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene) {
   if (!ctx) return RT_ERR_INVALID;
+  // multi-device: flattened and uploaded on every device concurrently
+  return fan_out(ctx, [&](int, rt_ctx* c) { return upload_one(c, scene); });
+}
+
+static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   free_scene(ctx);
@@ -675,8 +826,17 @@ int rt_render(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* pa
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(ctx->accum.p, accum_rgb, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
   double ms = 0.0;
-  rc = render_impl(ctx, cam, params, static_cast<float*>(ctx->accum.p), ctx->stream, false, nullptr, &ms);
-  if (rc) return rc;
+  if (ctx->subs.empty()) {
+    rc = render_impl(ctx, cam, params, static_cast<float*>(ctx->accum.p), ctx->stream, false, nullptr, &ms);
+    if (rc) return rc;
+  } else {
+    // every device writes its buckets into this device's frame
+    const auto t0 = std::chrono::steady_clock::now();
+    if ((rc = render_multi(ctx, cam, params, static_cast<float*>(ctx->accum.p), ctx->stream))) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if ((rc = rt_sync(ctx))) return rc;
+  }
   HIPCHK(hipMemcpyAsync(accum_rgb, ctx->accum.p, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (stats) {
@@ -699,25 +859,42 @@ int rt_render_device(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_par
   // next rt_sync / rt_last_render_kernel_ms)
   int rc = check_render_error(ctx, false);
   if (rc) return rc;
-  return render_impl(ctx, cam, params, accum_rgb_device, st, false, nullptr, nullptr);
+  if (ctx->subs.empty()) return render_impl(ctx, cam, params, accum_rgb_device, st, false, nullptr, nullptr);
+  for (rt_ctx* s : ctx->subs) {
+    HIPCHK(hipSetDevice(s->device));
+    if ((rc = check_render_error(s, false))) return set_err(ctx, rc, s->error);
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  return render_multi(ctx, cam, params, accum_rgb_device, st);
 }
 
 int rt_sync(rt_ctx* ctx) {
   if (!ctx) return RT_ERR_INVALID;
-  HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  return check_render_error(ctx, true);
+  return fan_out(ctx, [](int, rt_ctx* c) -> int {
+    rt_ctx* ctx = c;   // HIPCHK reports on this device's context
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return check_render_error(ctx, true);
+  });
 }
 
 int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms) {
   if (!ctx || !ms) return RT_ERR_INVALID;
-  HIPCHK(hipSetDevice(ctx->device));
-  if (!ctx->kev_recorded) return set_err(ctx, RT_ERR_INVALID, "no render recorded");
-  HIPCHK(hipEventSynchronize(ctx->kev1));
-  float f = 0.f;
-  HIPCHK(hipEventElapsedTime(&f, ctx->kev0, ctx->kev1));
-  *ms = f;
-  return check_render_error(ctx, true);
+  // multi-device: the slowest device's render kernels
+  std::vector<double> per(1 + ctx->subs.size(), -1.0);
+  int rc = fan_out(ctx, [&](int k, rt_ctx* c) -> int {
+    rt_ctx* ctx = c;
+    if (!ctx->kev_recorded) return RT_OK;
+    HIPCHK(hipEventSynchronize(ctx->kev1));
+    float f = 0.f;
+    HIPCHK(hipEventElapsedTime(&f, ctx->kev0, ctx->kev1));
+    per[size_t(k)] = f;
+    return check_render_error(ctx, true);
+  });
+  if (rc) return rc;
+  const double mx = *std::max_element(per.begin(), per.end());
+  if (mx < 0.0) return set_err(ctx, RT_ERR_INVALID, "no render recorded");
+  *ms = mx;
+  return RT_OK;
 }
 
 namespace {
@@ -832,6 +1009,33 @@ int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32
   HIPCHK(hipMemcpy(&flag, perr, sizeof(int), hipMemcpyDeviceToHost));
   if (flag) return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow");
   return RT_OK;
+}
+
+int rt_extend_first_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t* out_top,
+                         int32_t* out_prim, float* out_t) {
+  if (!ctx || !cam || !out_top || !out_prim || !out_t || sample < 0) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
+  const size_t n = size_t(cam->image_width) * cam->image_height;
+  int rc = ensure(ctx, ctx->accum, n * 3 * sizeof(float));
+  if (rc) return rc;
+  if ((rc = ensure(ctx, ctx->probe, n * 12))) return rc;
+  // one sample of every pixel, one bounce: the hit records of the first
+  // k_extend stay in the hit array (slot i = pixel list entry i)
+  const rt_render_params p{1, 1, sample, seed, nullptr, 0, 0};
+  rc = render_impl(ctx, cam, &p, static_cast<float*>(ctx->accum.p), ctx->stream, false, nullptr, nullptr);
+  if (rc) return rc;
+  int32_t* top = static_cast<int32_t*>(ctx->probe.p);
+  int32_t* prim = top + n;
+  float* t = reinterpret_cast<float*>(prim + n);
+  const float4* hit = static_cast<const float4*>(ctx->wstate.p) + 6 * ctx->wslots;   // WaveArgs::hit (render_wave)
+  HIPCHK(launch_hit_ids(ctx->dscene, hit, static_cast<const uint32_t*>(ctx->wpix.p), uint32_t(ctx->pix_host.size()),
+                        top, prim, t, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return check_render_error(ctx, true);
 }
 
 }  // extern "C"

@@ -421,7 +421,9 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
   float t1 = __builtin_inff(), t2 = __builtin_inff();
   bool h1 = false, h2 = false;
   constexpr int kCache = 6;   // a Box boundary: six quads
-  if (n <= kCache) {
+  // (a sphere's slot holds its index as an exact float value, not a bit
+  // pattern: below 2^24 every index is exact and no denormal is involved)
+  if (n <= kCache && sc.n_spheres < (1u << 24)) {
     // Only the two closest distances matter, and a quad's / triangle's hit
     // distance does not depend on the interval's lower bound (quad_t / tri_t
     // test it last): each is intersected once, with the bound -inf, and both
@@ -439,7 +441,7 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
       bool ok = false;
       if (pk == PK_QUAD) ok = quad_t(sc.quads[GIX(pi, sc.n_quads, 5)], o, d, ninf, tq[k]);
       else if (pk == PK_TRI) ok = tri_t(sc.tris[GIX(pi, sc.n_tris, 6)], o, d, ninf, tq[k]);
-      else if (pk == PK_SPHERE) { sph |= 1u << k; tq[k] = __uint_as_float(pi); }
+      else if (pk == PK_SPHERE) { sph |= 1u << k; tq[k] = float(pi); }
       if (ok) valid |= 1u << k;
     }
     for (int pass = 0; pass < 2; ++pass) {
@@ -451,7 +453,7 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
           if (lo <= tq[k] && tq[k] <= closest) { closest = tq[k]; found = true; }
         } else if ((sph >> k) & 1u) {
           float t = 0.0f;
-          if (sphere_t(sc.spheres[GIX(__float_as_uint(tq[k]), sc.n_spheres, 7)], o, d, time, lo, t) && t < closest) {
+          if (sphere_t(sc.spheres[GIX(uint32_t(tq[k]), sc.n_spheres, 7)], o, d, time, lo, t) && t < closest) {
             closest = t;
             found = true;
           }
@@ -657,6 +659,29 @@ constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackV
 #endif
 constexpr int kP2Slack = RTG_P2_SLACK;
 
+// Schedule independence of the closest hit (DESIGN §3 "Determinism").  The
+// result must not depend on which rays share a wave or on when a wave runs:
+//   * phase 1 is not speculative (RTG_P1_SPECULATE 0): a lane that reaches a
+//     leaf / instance item stops walking nodes until it has processed it, so
+//     every lane performs the sequential near-first traversal's operations in
+//     the same order whatever its wave-mates do (Aila & Laine's speculative
+//     walk tests nodes against a closest distance that depends on how long
+//     the wave stays in phase 1);
+//   * a box is culled against the closest distance widened by 2^-20
+//     (RTG_CULL_WIDEN): a primitive at t <= t_best whose box entry rounds a
+//     few ulps above t_best is still reached, so the box test never decides
+//     the winner.
+#ifndef RTG_P1_SPECULATE
+#define RTG_P1_SPECULATE 0
+#endif
+#ifndef RTG_CULL_WIDEN
+#define RTG_CULL_WIDEN 1
+#endif
+constexpr bool kP1Speculate = RTG_P1_SPECULATE != 0;
+__device__ __forceinline__ float cull_hi(float bt) {
+  return RTG_CULL_WIDEN ? bt * (1.0f + 0x1p-20f) : bt;   // +inf stays +inf
+}
+
 // accept() on the split record: a hit was accepted iff bt < tmax (the first
 // acceptance needs t < tmax), and the tie rule reads the LDS words.
 __device__ __forceinline__ bool accept_hit(const DScene& sc, float t, int kind, int refpos, int primpos, const Trav& T,
@@ -701,7 +726,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
   float tn = 0.0f;
   if (sc.tlas.check_box &&
       !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
-               T.cr, tmin, kAny ? tmax : T.bt, tn))
+               T.cr, tmin, kAny ? tmax : cull_hi(T.bt), tn))
     return TRAV_DONE;
   T.item = sc.tlas.root_item;
   if ((T.item >> ITEM_SHIFT) != ITEM_NODE) {
@@ -729,9 +754,12 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     S.push(T.sp, v, err);
     ++T.sp;
   };
+  // postpone the current leaf / instance item; the speculative variant pops
+  // the next stack entry and keeps walking nodes (leaves only: entering an
+  // instance changes the stack)
   auto postpone = [&]() {
     T.lf = T.item;
-    T.item = item_is_leaf(T.lf) ? pop() : ITEM_POP;
+    T.item = (kP1Speculate && item_is_leaf(T.lf)) ? pop() : ITEM_POP;
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
@@ -739,7 +767,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const bool st_lead = rtg_lead();
     const uint32_t st0 = rtg_stamp();
 #endif
-    const float hi = kAny ? T.tmax : T.bt;
+    const float hi = kAny ? T.tmax : cull_hi(T.bt);
     const float inf = __builtin_inff();
     const uint32_t nidx = GIX(T.item & ITEM_MASK, sc.n_nodes, 9);
     float t0, t1, t2, t3;
@@ -936,11 +964,16 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           const float4 lo = bp[0], hi = bp[1];
           float tn = 0.0f;
           if (kCount) cnt.ibox++;
-          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : T.bt, tn)) continue;
+          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : cull_hi(T.bt), tn)) continue;
           push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos));
           continue;
         } else if (kVol && pk == PK_VOLUME) {
-          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), S.time(), T.tmin, kAny ? T.tmax : T.bt,
+          // Closest hit: the free flight is measured over the ray's whole
+          // interval and the hit then competes like any other (accept_hit).
+          // Volume.Hit clamps t2 to the closest distance so far
+          // (volume.go:52-54), which selects the same winner up to rounding
+          // but would make the result depend on the visiting order.
+          ok = volume_hit<kCount>(sc, sc.volumes[GIX(pi, sc.n_volumes, 16)], S.wo(), S.wd(), S.time(), T.tmin, T.tmax,
                                   leaf_ntests(leaf.info), T.key, T.bounce, T.voldom, t, cnt);
         }
         if (!ok) continue;
@@ -986,7 +1019,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       // several objects was culled there), then the wrapper chain (the ray
       // into object space, transform.go) and the BLAS root box.
       const bool winst = tag == ITEM_WINST;
-      const float hi = kAny ? T.tmax : T.bt;
+      const float hi = kAny ? T.tmax : cull_hi(T.bt);
       float tn = 0.0f;
       bool go = true;
       if (winst) {

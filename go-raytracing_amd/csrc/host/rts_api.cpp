@@ -96,6 +96,9 @@ struct rts_renderer {
   int current_pass = 0;
   bool completed = false;
   std::chrono::steady_clock::time_point start = std::chrono::steady_clock::now(), end;
+  double create_ms = 0.0;                  // context + scene upload (flatten, BVH builds)
+  double pass_wall_ms[3] = {0, 0, 0};      // each pass: rt_render + tonemap, host clock
+  double pass_render_ms[3] = {0, 0, 0};    // each pass: rt_render's device time (rt_stats.kernel_ms)
   std::string error;
 };
 
@@ -164,7 +167,19 @@ int rts_renderer_create(const rts_scene* s, int32_t bucket_size, int32_t num_wor
   r->s = s;
   r->bucket_size = bucket_size;
   r->seed = seed;
-  int rc = rt_ctx_create(device, &r->ctx);
+  // device < 0: every visible device (the worker pool of NumCPU goroutines,
+  // main.go:84, becomes one GPU per worker: rt_ctx_create_multi)
+  int rc;
+  if (device < 0) {
+    int32_t n = 0;
+    rc = rt_device_count(&n);
+    if (!rc && n <= 0) rc = RT_ERR_HIP;
+    std::vector<int32_t> devs;
+    for (int32_t d = 0; d < n; ++d) devs.push_back(d);
+    if (!rc) rc = rt_ctx_create_multi(devs.data(), n, &r->ctx);
+  } else {
+    rc = rt_ctx_create(device, &r->ctx);
+  }
   if (rc) { copy_err(err, errlen, "rt_ctx_create failed"); delete r; return rc; }
   rc = rt_scene_upload(r->ctx, &s->desc);
   if (rc) { copy_err(err, errlen, rt_last_error(r->ctx)); rt_ctx_destroy(r->ctx); delete r; return rc; }
@@ -180,7 +195,7 @@ int rts_renderer_create(const rts_scene* s, int32_t bucket_size, int32_t num_wor
   });
   r->accum.assign(size_t(W) * H * 3, 0.f);
   r->framebuffer.assign(size_t(W) * H * 4, 0);
-  r->start = std::chrono::steady_clock::now();
+  r->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r->start).count();
   *out = r;
   return RT_OK;
 }
@@ -208,10 +223,16 @@ int rts_renderer_render_pass(rts_renderer* r, int32_t pass) {
   p.buckets = r->buckets.data();
   p.num_buckets = int32_t(r->buckets.size());
   p.accumulate = 0;   // each pass overwrites (renderBucketWithQuality)
-  int rc = rt_render(r->ctx, &c, &p, r->accum.data(), nullptr);
+  const auto t0 = std::chrono::steady_clock::now();
+  rt_stats st{};
+  int rc = rt_render(r->ctx, &c, &p, r->accum.data(), &st);
   if (rc) { r->error = rt_last_error(r->ctx); return rc; }
   rc = rt_tonemap_rgba8(r->ctx, r->accum.data(), c.image_width, c.image_height, spp, r->framebuffer.data());
   if (rc) { r->error = rt_last_error(r->ctx); return rc; }
+  if (pass >= 0 && pass < 3) {
+    r->pass_render_ms[pass] = st.kernel_ms;
+    r->pass_wall_ms[pass] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
   r->current_pass = pass + 1;
   if (pass >= 2) {
     r->completed = true;
@@ -241,6 +262,12 @@ int rts_renderer_save_png(const rts_renderer* r, const char* path) {
   return write_png(path, r->framebuffer.data(), r->s->cam.image_width, r->s->cam.image_height) ? RT_OK : RT_ERR_INVALID;
 }
 const char* rts_renderer_last_error(const rts_renderer* r) { return r ? r->error.c_str() : "null renderer"; }
+int rts_renderer_timings(const rts_renderer* r, double out[7]) {
+  if (!r || !out) return RT_ERR_INVALID;
+  out[0] = r->create_ms;
+  for (int k = 0; k < 3; ++k) { out[1 + k] = r->pass_wall_ms[k]; out[4 + k] = r->pass_render_ms[k]; }
+  return RT_OK;
+}
 
 int rts_load_hdr(const char* path, int32_t* width, int32_t* height, double* rgb_out, int64_t cap) {
   if (!path) return RT_ERR_INVALID;

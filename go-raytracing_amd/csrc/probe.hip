@@ -37,6 +37,34 @@ __global__ void tonemap_kernel(const float* accum, int n, int spp, uint8_t* rgba
   reinterpret_cast<uchar4*>(rgba)[i] = make_uchar4(o[0], o[1], o[2], o[3]);
 }
 
+// Hittable ids of a closest hit (kind, primitive index, TLAS ref position).
+__device__ __forceinline__ void hit_ids(const DScene& sc, int kind, int idx, int refpos, int& top, int& prim) {
+  if (kind == PK_PLANE) { top = prim = sc.plane_hidx[idx]; return; }
+  top = sc.tlas_ref_top[refpos];
+  if (kind == PK_SPHERE) prim = sc.sphere_hidx[idx];
+  else if (kind == PK_QUAD) prim = sc.quad_hidx[idx];
+  else if (kind == PK_TRI) prim = sc.tri_hidx[idx];
+  else if (kind == PK_CIRCLE) prim = sc.circle_hidx[idx];
+  else prim = sc.volume_hidx[idx];
+}
+
+// rt_extend_first_hits: k_extend's hit records (wavefront.hip store_hit:
+// t, kind<<28|idx, instance, refpos) of the pixel list -> ids per pixel.
+__global__ __launch_bounds__(256) void hit_ids_kernel(DScene sc, const float4* hit, const uint32_t* pixels,
+                                                      uint32_t npix, int32_t* out_top, int32_t* out_prim,
+                                                      float* out_t) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= npix) return;
+  const float4 h = hit[i];
+  const uint32_t kh = __float_as_uint(h.y);
+  int top = -1, prim = -1;
+  if (kh != 0u) hit_ids(sc, int(kh >> 28), int(kh & 0x0FFFFFFFu), int(__float_as_uint(h.w)), top, prim);
+  const uint32_t p = pixels[i];
+  out_top[p] = top;
+  out_prim[p] = prim;
+  out_t[p] = kh ? h.x : -1.0f;
+}
+
 // Parity probe: first-bounce closest hit of one sample per pixel.
 template <int STACK, bool kQuant>
 __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, uint32_t seed, int sample,
@@ -55,17 +83,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DScene sc, DCamera cam, ui
   bool hit = traverse<false, false, true, kQuant>(sc, ro, rd, time, 0.001f, __builtin_inff(), lds_stack_only(lds_stack + tid, 256, STACK), b, key,
                                     0, DOM_VOL, cnt, err);
   int top = -1, prim = -1;
-  if (hit) {
-    if (b.kind == PK_PLANE) { top = prim = sc.plane_hidx[b.idx]; }
-    else {
-      top = sc.tlas_ref_top[b.refpos];
-      if (b.kind == PK_SPHERE) prim = sc.sphere_hidx[b.idx];
-      else if (b.kind == PK_QUAD) prim = sc.quad_hidx[b.idx];
-      else if (b.kind == PK_TRI) prim = sc.tri_hidx[b.idx];
-      else if (b.kind == PK_CIRCLE) prim = sc.circle_hidx[b.idx];
-      else prim = sc.volume_hidx[b.idx];
-    }
-  }
+  if (hit) hit_ids(sc, b.kind, b.idx, b.refpos, top, prim);
   out_top[i] = top;
   out_prim[i] = prim;
   out_t[i] = hit ? b.t : -1.0f;
@@ -91,6 +109,14 @@ hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, i
     if (q) hipLaunchKernelGGL((primary_kernel<64, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
     else hipLaunchKernelGGL((primary_kernel<64, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_hit_ids(const DScene& sc, const float4* hit, const uint32_t* pixels, uint32_t npix, int32_t* top,
+                          int32_t* prim, float* t, hipStream_t st) {
+  if (npix == 0) return hipSuccess;
+  hipLaunchKernelGGL(hit_ids_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, st, sc, hit, pixels, npix, top, prim,
+                     t);
   return hipGetLastError();
 }
 

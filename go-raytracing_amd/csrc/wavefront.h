@@ -67,6 +67,7 @@ struct WavePlan {
   uint32_t sample_offset;
   int32_t max_depth;
   int32_t num_cus;
+  int32_t max_blocks;       // > 0: cap on the persistent traversal grids (RT_OPT_MAX_BLOCKS)
   uint32_t* probe_host;     // pinned word for the long-tail early exit
   // Per-launch timing (rt_set_kernel_timing): an event is recorded before
   // every extend/shade/shadow launch and after every shadow launch;

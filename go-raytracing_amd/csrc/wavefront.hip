@@ -166,10 +166,12 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   return idx;
 }
 
+// Hit record: t, kind<<28 | idx (0 = miss), instance, TLAS ref position (the
+// top-level object: read by the rt_extend_first_hits parity probe only).
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
   stnt(&hit[p], make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
-                       0.0f));
+                       asf(uint32_t(b.refpos))));
 }
 
 // ---------------------------------------------------------------- extend
@@ -706,7 +708,9 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
     const uint32_t sample_base = plan.sample_offset + s0;
     hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, a.counts, nslots);
     if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
-    const int max_trav_blocks = int(a.spill_lanes / 256u);   // one spill column per resident lane
+    // one spill column per resident lane; RT_OPT_MAX_BLOCKS may cap it further
+    int max_trav_blocks = int(a.spill_lanes / 256u);
+    if (plan.max_blocks > 0 && plan.max_blocks < max_trav_blocks) max_trav_blocks = plan.max_blocks;
     const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, 0, nslots, cus);
     int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus);
     gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;

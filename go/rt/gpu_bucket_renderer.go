@@ -23,11 +23,6 @@ import (
 	"go-raytracing/rtgpu"
 )
 
-// gpuChunkBuckets is how many buckets one rt_render call takes: a chunk of
-// 64 32x32 buckets is ~65K pixels (enough to fill the GPU at 1 spp) and
-// keeps the window's progress bar moving during a long pass.
-const gpuChunkBuckets = 64
-
 // GPUBucketRenderer is a BucketRenderer whose passes run on the GPU.  When
 // the scene holds something the GPU path does not take (rtgpu.IsUnsupported)
 // or no device is present, gpu is nil and every method is the CPU
@@ -40,11 +35,13 @@ type GPUBucketRenderer struct {
 	accum   []float32      // per-pixel radiance sums of the pass in flight
 	rgba    []byte         // tonemapped frame of the pass in flight
 	seed    uint32
-	err     error // first GPU error; the render stops there
+	err     error // first GPU error (under BucketRenderer.mu); the render stops there
 }
 
 // NewGPUBucketRenderer has NewBucketRenderer's signature
-// (bucket_renderer.go:54-74); numWorkers only matters for the CPU fallback.
+// (bucket_renderer.go:54-74).  Its worker pool is every visible GPU (as
+// main.go:84 sizes the CPU pool with runtime.NumCPU()); numWorkers only
+// matters for the CPU fallback.
 func NewGPUBucketRenderer(camera *Camera, world Hittable, bucketSize int, numWorkers int) *GPUBucketRenderer {
 	g := &GPUBucketRenderer{BucketRenderer: NewBucketRenderer(camera, world, bucketSize, numWorkers), seed: 1}
 	if err := g.initGPU(camera, world); err != nil {
@@ -63,7 +60,7 @@ func (g *GPUBucketRenderer) initGPU(camera *Camera, world Hittable) error {
 	if err != nil {
 		return err
 	}
-	if g.gpu, err = rtgpu.New(0); err != nil {
+	if g.gpu, err = rtgpu.New(); err != nil { // every visible device
 		return err
 	}
 	if err = g.gpu.Upload(scene); err != nil {
@@ -110,13 +107,14 @@ func (g *GPUBucketRenderer) Update() error {
 		r.passComplete.Store(false)
 		r.completedCount.Store(0)
 		r.currentPass++
-		if r.currentPass < r.totalPasses && g.err == nil {
+		gerr := g.passErr()
+		if r.currentPass < r.totalPasses && gerr == nil {
 			go g.gpuPass()
 		} else {
 			r.completed = true
 			r.renderEnd = time.Now()
-			if g.err != nil {
-				fmt.Fprintf(os.Stderr, "GPU render failed: %v\n", g.err)
+			if gerr != nil {
+				fmt.Fprintf(os.Stderr, "GPU render failed: %v\n", gerr)
 			}
 			r.drawStatsToFramebuffer()
 			_ = r.SaveImage("image.png")
@@ -139,37 +137,42 @@ func passQuality(pass int, c *Camera) (spp, depth int) {
 	}
 }
 
-// gpuPass renders the current pass chunk by chunk in bucket order; each
-// chunk overwrites its buckets' sums (renderBucketWithQuality writes every
-// bucket pixel each pass), is tonemapped on the device with
-// bucket_renderer.go:276-285's quantisation and copied into the
+// passErr is the first GPU error so far; gpuPass writes it under r.mu on its
+// goroutine, Update reads it on the game loop's.
+func (g *GPUBucketRenderer) passErr() error {
+	g.BucketRenderer.mu.Lock()
+	defer g.BucketRenderer.mu.Unlock()
+	return g.err
+}
+
+// gpuPass renders the current pass in one call over every device (each
+// render deals the buckets round-robin over the context's GPUs and
+// overwrites their sums, as renderBucketWithQuality writes every bucket
+// pixel each pass), tonemaps the frame once on the device with
+// bucket_renderer.go:276-285's quantisation and copies it into the
 // framebuffer bucket by bucket under r.mu, as renderBucketWithQuality does.
 func (g *GPUBucketRenderer) gpuPass() {
 	r := g.BucketRenderer
 	spp, depth := passQuality(r.currentPass, r.camera)
 	w, h := r.camera.ImageWidth, r.camera.ImageHeight
 	seed := g.seed + uint32(r.currentPass)*0x9E3779B9 // one RNG stream per pass
-	for lo := 0; lo < len(g.buckets) && g.err == nil; lo += gpuChunkBuckets {
-		hi := min(lo+gpuChunkBuckets, len(g.buckets))
-		chunk := g.buckets[lo:hi]
-		_, err := g.gpu.Render(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
-			Buckets: chunk}, g.accum)
-		if err == nil {
-			err = g.gpu.Tonemap(g.accum, w, h, spp, g.rgba)
-		}
-		if err != nil {
-			g.err = err
-			break
-		}
-		r.mu.Lock()
-		for _, b := range chunk {
+	_, err := g.gpu.Render(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
+		Buckets: g.buckets}, g.accum)
+	if err == nil {
+		err = g.gpu.Tonemap(g.accum, w, h, spp, g.rgba)
+	}
+	r.mu.Lock()
+	if err != nil {
+		g.err = err
+	} else {
+		for _, b := range g.buckets {
 			for y := int(b.Y); y < int(b.Y+b.Height); y++ {
 				row := (y*w + int(b.X)) * 4
 				copy(r.framebuffer.Pix[row:row+int(b.Width)*4], g.rgba[row:row+int(b.Width)*4])
 			}
 		}
-		r.mu.Unlock()
-		r.completedCount.Add(int32(len(chunk)))
 	}
+	r.mu.Unlock()
+	r.completedCount.Add(int32(len(g.buckets)))
 	r.passComplete.Store(true)
 }

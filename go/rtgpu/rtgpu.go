@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the RT_ABI_VERSION this binding was written against.
-const ABIVersion = 4 // RT_ABI_VERSION
+const ABIVersion = 5 // RT_ABI_VERSION
 
 // Hittable kinds (enum rt_hittable_kind).
 const (
@@ -263,22 +263,62 @@ func IsUnsupported(err error) bool {
 	return errors.As(err, &e) && e.Status == StatusUnsupported
 }
 
-// Ctx is one device context (rt_ctx).  Not safe for concurrent use.
+// Ctx is a context over one or several devices (rt_ctx).  Not safe for
+// concurrent use.
 type Ctx struct {
 	p *C.rt_ctx
 }
 
-// New creates a context on HIP device `device` after checking the ABI.
-func New(device int) (*Ctx, error) {
+// DeviceCount is the number of visible HIP devices (rt_device_count).
+func DeviceCount() (int, error) {
+	var n C.int32_t
+	if rc := C.rt_device_count(&n); rc != C.RT_OK {
+		return 0, &Error{int(rc), "rt_device_count failed"}
+	}
+	return int(n), nil
+}
+
+// New creates a context after checking the ABI: on HIP device devices[0]
+// alone, or over every listed device (rt_ctx_create_multi: each render deals
+// its buckets round-robin over them, like bucket_renderer.go:193-213's
+// worker pool with one GPU per worker).  No devices: every visible device.
+func New(devices ...int) (*Ctx, error) {
 	if v := int(C.rt_abi_version()); v != ABIVersion {
 		return nil, &Error{StatusInvalid, fmt.Sprintf("librtgpu ABI %d, binding expects %d", v, ABIVersion)}
 	}
+	if len(devices) == 0 {
+		n, err := DeviceCount()
+		if err != nil {
+			return nil, err
+		}
+		if n == 0 {
+			return nil, &Error{StatusHIP, "no HIP device"}
+		}
+		for d := 0; d < n; d++ {
+			devices = append(devices, d)
+		}
+	}
 	var p *C.rt_ctx
-	if rc := C.rt_ctx_create(C.int(device), &p); rc != C.RT_OK {
-		return nil, &Error{int(rc), "rt_ctx_create failed"}
+	if len(devices) == 1 {
+		if rc := C.rt_ctx_create(C.int(devices[0]), &p); rc != C.RT_OK {
+			return nil, &Error{int(rc), "rt_ctx_create failed"}
+		}
+		return &Ctx{p: p}, nil
+	}
+	list := (*C.int32_t)(C.calloc(C.size_t(len(devices)), C.sizeof_int32_t))
+	defer C.free(unsafe.Pointer(list))
+	ids := unsafe.Slice(list, len(devices))
+	for i, d := range devices {
+		ids[i] = C.int32_t(d)
+	}
+	if rc := C.rt_ctx_create_multi(list, C.int32_t(len(devices)), &p); rc != C.RT_OK {
+		return nil, &Error{int(rc), "rt_ctx_create_multi failed"}
 	}
 	return &Ctx{p: p}, nil
 }
+
+// NumDevices is the number of devices the context renders on.
+func (c *Ctx) NumDevices() int { return int(C.rt_ctx_num_devices(c.p)) }
 
 // Close releases the context and its device memory.
 func (c *Ctx) Close() {

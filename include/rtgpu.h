@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -245,6 +245,26 @@ int rt_ctx_create(int device, rt_ctx** out);
 void rt_ctx_destroy(rt_ctx* ctx);
 const char* rt_last_error(const rt_ctx* ctx);
 
+/* Visible HIP devices (what the Go side passes as the device list, the way
+ * main.go:84 sizes the worker pool with runtime.NumCPU()).                 */
+int rt_device_count(int32_t* num_devices);
+
+/* One context over several devices (bucket_renderer.go:193-213's worker
+ * pool with one GPU per worker).  devices[0] is the primary: the frame of
+ * rt_render_device must live there, and rt_render stages through it.
+ * rt_scene_upload flattens and uploads on every device concurrently;
+ * rt_render / rt_render_device deal the buckets round-robin over the devices
+ * (bucket k -> device k mod n) and render every share at once, one host
+ * thread per device; each device writes its own pixels straight into the
+ * primary's frame (peer access over xGMI), so the frame is bit-identical to a
+ * one-device render.  rt_render_device stays asynchronous on the caller's
+ * stream.  rt_ctx_set_option / rt_sync / rt_last_render_kernel_ms (the
+ * slowest device) cover every device; the probes, counters, per-launch
+ * timing and tonemap run on the primary only.  A device list may repeat a
+ * device.  RT_ERR_UNSUPPORTED: a device without peer access to devices[0]. */
+int rt_ctx_create_multi(const int32_t* devices, int32_t num_devices, rt_ctx** out);
+int rt_ctx_num_devices(const rt_ctx* ctx);
+
 /* Context options (take effect at the next rt_scene_upload).
  *   RT_OPT_BLAS_BUILDER: how an all-triangle mesh BVH (LoadOBJ ->
  *     NewBVHNode, obj_loader.go:109) is laid out on the device:
@@ -267,7 +287,16 @@ const char* rt_last_error(const rt_ctx* ctx);
  *     the same closest hits).  Scenes holding a RotateX/RotateZ wrapper
  *     always use RT_NODES_FP32 (their node boxes decide which rays reach
  *     an object, transform.go:201-351).                                   */
-enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3 };
+/* Schedule options (take effect at the next render; 0 = automatic).  They
+ * change how the work is dealt to the GPU, never the image: the closest hit
+ * is independent of the traversal schedule.
+ *   RT_OPT_BATCH_SLOTS: path slots per batch (default: from half the free
+ *     HBM, at most 512M).
+ *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
+ *     of rays (default 16).
+ *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups). */
+enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
+       RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);
@@ -334,6 +363,12 @@ int rt_tonemap_rgba8(rt_ctx* ctx, const float* accum_rgb, int32_t width, int32_t
  * non-instanced objects), -1 on miss; out_t = hit distance.               */
 int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
                     int32_t* out_top, int32_t* out_prim, float* out_t);
+
+/* The same ids from the production pipeline: the hit records the render's
+ * first-bounce closest-hit kernel (k_extend, persistent, with the context's
+ * schedule options) writes for sample `sample` of every pixel.            */
+int rt_extend_first_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
+                         int32_t* out_top, int32_t* out_prim, float* out_t);
 
 #ifdef __cplusplus
 }

@@ -49,8 +49,10 @@ const rt_camera_desc* rts_scene_get_camera(const rts_scene* s);
 /* world.Objects (pre-BVH list order) as hittable indices; returns count. */
 int32_t rts_scene_world_objects(const rts_scene* s, int32_t* out, int32_t cap);
 
-/* NewBucketRenderer(camera, world, bucketSize, numWorkers) on GPU `device`.
- * numWorkers is accepted for signature parity (the GPU schedules itself). */
+/* NewBucketRenderer(camera, world, bucketSize, numWorkers) on GPU `device`
+ * (device < 0: every visible GPU, one multi-device context).  numWorkers is
+ * accepted for signature parity (the GPU schedules itself).  The duration
+ * clock starts here, as bucket_renderer.go:68's renderStart does.        */
 typedef struct rts_renderer rts_renderer;
 int rts_renderer_create(const rts_scene* s, int32_t bucket_size, int32_t num_workers, int32_t device, uint32_t seed,
                         rts_renderer** out, char* err, int32_t errlen);
@@ -65,6 +67,10 @@ const float* rts_renderer_accum(const rts_renderer* r);         /* last pass sum
 double rts_renderer_duration_ms(const rts_renderer* r);
 int rts_renderer_save_png(const rts_renderer* r, const char* path);
 const char* rts_renderer_last_error(const rts_renderer* r);
+/* out[0] = construction ms (context + scene upload), out[1..3] = each pass's
+ * wall ms (rt_render with host buffers + tonemap), out[4..6] = each pass's
+ * device render ms (rt_stats.kernel_ms).                                  */
+int rts_renderer_timings(const rts_renderer* r, double out[7]);
 
 /* Loader probes (HDR: image_loader.go:165-383; OBJ: obj_loader.go:15-113). */
 int rts_load_hdr(const char* path, int32_t* width, int32_t* height, double* rgb_out /* may be NULL */,
