@@ -480,24 +480,34 @@ def main():
     if D.world == 1 and devices is None and not args.no_balance:
         import torch
 
-        def timed_render(params) -> float:
+        w.ctx.set_kernel_timing(True)
+
+        def timed_render(params):
+            """(host ms around render + sync, device ms of the render kernels,
+            summed extend/shade/shadow launch ms)"""
             w.accum.zero_()
             torch.cuda.synchronize(D.dev)
             t0 = time.perf_counter()
             w.ctx.render_device(w.cam, params, w.accum.data_ptr(), w.stream.cuda_stream)
             w.ctx.sync()
-            return (time.perf_counter() - t0) * 1e3
+            host = (time.perf_counter() - t0) * 1e3
+            kt = w.ctx.last_kernel_times()
+            return host, w.ctx.last_render_kernel_ms(), kt["extend_ms"] + kt["shade_ms"] + kt["shadow_ms"]
 
         full = min(timed_render(w.params) for _ in range(2))
-        balance = {"full_frame_ms": round(full, 2)}
+        balance = {"full_frame_ms": round(full[0], 2), "full_frame_device_ms": round(full[1], 2),
+                   "full_frame_trav_shade_ms": round(full[2], 2)}
         for n in (2, 4, 8):
-            shard_ms = []
+            runs = []
             for r in range(n):
                 p = g.make_params(spp, depth, seed=args.seed, buckets=g.shard_buckets(w.buckets, r, n))
-                shard_ms.append(min(timed_render(p) for _ in range(2)))
+                runs.append(min(timed_render(p) for _ in range(2)))
+            shard_ms = [x[0] for x in runs]
             mx, mean = max(shard_ms), float(np.mean(shard_ms))
             balance[f"n{n}"] = {"shard_ms": [round(x, 2) for x in shard_ms], "max_over_mean": round(mx / mean, 4),
-                                "predicted_speedup": round(full / mx, 3)}
+                                "predicted_speedup": round(full[0] / mx, 3),
+                                "shard_device_ms": [round(x[1], 2) for x in runs],
+                                "shard_trav_shade_ms": [round(x[2], 2) for x in runs]}
         balance["note"] = ("round-robin 32x32 bucket shards (shard_buckets) timed one after another on this GPU, "
                            "host clock around render + sync; predicted speed-up = full frame / slowest shard, "
                            "excluding the RCCL reduce of the frame")

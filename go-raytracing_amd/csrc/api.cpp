@@ -329,6 +329,11 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   a.refill = ctx->opt_refill ? ctx->opt_refill : refill;
   WavePlan plan{};
   plan.max_blocks = ctx->opt_blocks;
+  static const int debug_sync = [] {
+    const char* e = getenv("RTGPU_DEBUG_SYNC");
+    return e && atoi(e) > 0 ? 1 : 0;
+  }();
+  plan.debug_sync = debug_sync;
   plan.spp = spp;
   plan.samples_per_batch = spb;
   plan.sample_offset = uint32_t(p->sample_offset);

@@ -623,8 +623,10 @@ struct Trav {
   uint32_t key, bounce, voldom;
   uint32_t item, lf;
   int sp;                // the ray time and the current instance ref are in LDS (TStack)
-  float bt;              // closest accepted hit distance (tmax: none); the rest of the
-                         // hit record is in LDS (TStack::set_hit)
+  float bt;              // the box-cull bound: the closest accepted hit distance (tmax:
+                         // none) widened by cull_widen; best_t(T) recovers the exact
+                         // distance from its bits.  The rest of the hit record is in
+                         // LDS (TStack::set_hit)
 };
 
 // Best.primpos flags: bit 31 = mixed-leaf ref position, bit 30 = the hit lies
@@ -661,16 +663,17 @@ constexpr int kP2Slack = RTG_P2_SLACK;
 
 // Schedule independence of the closest hit (DESIGN §3 "Determinism").  The
 // result must not depend on which rays share a wave or on when a wave runs:
-//   * phase 1 is not speculative (RTG_P1_SPECULATE 0): a lane that reaches a
-//     leaf / instance item stops walking nodes until it has processed it, so
+//   * closest-hit phase 1 is not speculative (RTG_P1_SPECULATE 0): a lane
+//     that reaches a leaf / instance item stops walking nodes until it has
+//     processed it, so
 //     every lane performs the sequential near-first traversal's operations in
 //     the same order whatever its wave-mates do (Aila & Laine's speculative
 //     walk tests nodes against a closest distance that depends on how long
 //     the wave stays in phase 1);
-//   * a box is culled against the closest distance widened by 2^-20
-//     (RTG_CULL_WIDEN): a primitive at t <= t_best whose box entry rounds a
-//     few ulps above t_best is still reached, so the box test never decides
-//     the winner.
+//   * a box is culled against the closest distance widened by 8 ulps
+//     (RTG_CULL_WIDEN, cull_widen): a primitive at t <= t_best whose box
+//     entry rounds a few ulps above t_best is still reached, so the box test
+//     never decides the winner.
 #ifndef RTG_P1_SPECULATE
 #define RTG_P1_SPECULATE 0
 #endif
@@ -678,26 +681,44 @@ constexpr int kP2Slack = RTG_P2_SLACK;
 #define RTG_CULL_WIDEN 1
 #endif
 constexpr bool kP1Speculate = RTG_P1_SPECULATE != 0;
-__device__ __forceinline__ float cull_hi(float bt) {
-  return RTG_CULL_WIDEN ? bt * (1.0f + 0x1p-20f) : bt;   // +inf stays +inf
+// The widened bound is what the closest-hit register T.bt holds, so the node
+// loop culls against it with no extra instruction (a multiply there cost 7
+// VGPR spills at the 72-register cap, 4 % of the frame): 8 ulps above the
+// exact distance, as bits, so the exact value comes back by a subtraction.
+// Positive finite distances only (t >= tmin > 0); +inf stays +inf (a bit
+// pattern past +inf would be a NaN, which fmaxf / fminf would not ignore
+// the same way on every path).
+constexpr uint32_t kCullUlps = RTG_CULL_WIDEN ? 8u : 0u;
+__device__ __forceinline__ float cull_widen(float t) {
+  const uint32_t b = __float_as_uint(t);
+  const uint32_t w = b + kCullUlps;
+  return b >= 0x7F800000u ? t : __uint_as_float(w < 0x7F800000u ? w : 0x7F800000u);
 }
+__device__ __forceinline__ float cull_exact(float w) {
+  const uint32_t b = __float_as_uint(w);
+  return b >= 0x7F800000u ? w : __uint_as_float(b - kCullUlps);
+}
+__device__ __forceinline__ float best_t(const Trav& T) { return cull_exact(T.bt); }
 
-// accept() on the split record: a hit was accepted iff bt < tmax (the first
-// acceptance needs t < tmax), and the tie rule reads the LDS words.
+// accept() on the split record: a hit was accepted iff the exact closest
+// distance is below tmax (the first acceptance needs t < tmax), and the tie
+// rule reads the LDS words.
 __device__ __forceinline__ bool accept_hit(const DScene& sc, float t, int kind, int refpos, int primpos, const Trav& T,
                                            const TStack& S) {
-  if (t < T.bt) return true;
-  if (t == T.bt && T.bt < T.tmax) return tie_wins(sc, kind, refpos, primpos, S.hit_kind(), S.hit_refpos(), S.hit_primpos());
+  if (!(t <= T.bt)) return false;   // beyond the widened bound: beyond the exact one
+  const float bt = best_t(T);
+  if (t < bt) return true;
+  if (t == bt && bt < T.tmax) return tie_wins(sc, kind, refpos, primpos, S.hit_kind(), S.hit_refpos(), S.hit_primpos());
   return false;
 }
 __device__ __forceinline__ void take_hit(Trav& T, const TStack& S, float t, int kind, int idx, int refpos, int primpos) {
-  T.bt = t;
+  T.bt = cull_widen(t);
   S.set_hit(kind, idx, refpos, primpos);
 }
 // The finished ray's record (inst resolved by the caller, resolve_inst).
 __device__ __forceinline__ Best trav_best(const Trav& T, const TStack& S) {
   Best b;
-  b.t = T.bt; b.inst = -1;
+  b.t = best_t(T); b.inst = -1;
   b.kind = S.hit_kind(); b.idx = S.hit_idx(); b.refpos = S.hit_refpos(); b.primpos = S.hit_primpos();
   return b;
 }
@@ -709,7 +730,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
                                          Cnt& cnt) {
   S.set_time(time); T.tmin = tmin; T.tmax = tmax;
   T.key = key; T.bounce = bounce; T.voldom = voldom;
-  T.bt = tmax;
+  T.bt = cull_widen(tmax);
   if (!kAny) S.set_hit(0, -1, 0, 0);
   for (int i = 0; i < sc.num_planes; ++i) {
     float t = 0.0f;
@@ -726,7 +747,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
   float tn = 0.0f;
   if (sc.tlas.check_box &&
       !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
-               T.cr, tmin, kAny ? tmax : cull_hi(T.bt), tn))
+               T.cr, tmin, kAny ? tmax : T.bt, tn))
     return TRAV_DONE;
   T.item = sc.tlas.root_item;
   if ((T.item >> ITEM_SHIFT) != ITEM_NODE) {
@@ -756,10 +777,11 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
   };
   // postpone the current leaf / instance item; the speculative variant pops
   // the next stack entry and keeps walking nodes (leaves only: entering an
-  // instance changes the stack)
+  // instance changes the stack).  Any-hit rays always speculate: their result
+  // (is there a hit in [tmin, tmax]) does not depend on the visiting order.
   auto postpone = [&]() {
     T.lf = T.item;
-    T.item = (kP1Speculate && item_is_leaf(T.lf)) ? pop() : ITEM_POP;
+    T.item = ((kP1Speculate || kAny) && item_is_leaf(T.lf)) ? pop() : ITEM_POP;
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
@@ -767,7 +789,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const bool st_lead = rtg_lead();
     const uint32_t st0 = rtg_stamp();
 #endif
-    const float hi = kAny ? T.tmax : cull_hi(T.bt);
+    const float hi = kAny ? T.tmax : T.bt;
     const float inf = __builtin_inff();
     const uint32_t nidx = GIX(T.item & ITEM_MASK, sc.n_nodes, 9);
     float t0, t1, t2, t3;
@@ -964,7 +986,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           const float4 lo = bp[0], hi = bp[1];
           float tn = 0.0f;
           if (kCount) cnt.ibox++;
-          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : cull_hi(T.bt), tn)) continue;
+          if (!box_hit(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, T.cr, T.tmin, kAny ? T.tmax : T.bt, tn)) continue;
           push((ITEM_INSTANCE << ITEM_SHIFT) | uint32_t(pos));
           continue;
         } else if (kVol && pk == PK_VOLUME) {
@@ -1019,7 +1041,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       // several objects was culled there), then the wrapper chain (the ray
       // into object space, transform.go) and the BLAS root box.
       const bool winst = tag == ITEM_WINST;
-      const float hi = kAny ? T.tmax : cull_hi(T.bt);
+      const float hi = kAny ? T.tmax : T.bt;
       float tn = 0.0f;
       bool go = true;
       if (winst) {

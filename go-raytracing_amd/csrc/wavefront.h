@@ -68,6 +68,7 @@ struct WavePlan {
   int32_t max_depth;
   int32_t num_cus;
   int32_t max_blocks;       // > 0: cap on the persistent traversal grids (RT_OPT_MAX_BLOCKS)
+  int32_t debug_sync;       // RTGPU_DEBUG_SYNC=1: synchronise after every launch, name a failing kernel
   uint32_t* probe_host;     // pinned word for the long-tail early exit
   // Per-launch timing (rt_set_kernel_timing): an event is recorded before
   // every extend/shade/shadow launch and after every shadow launch;

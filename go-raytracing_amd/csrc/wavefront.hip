@@ -20,6 +20,7 @@
 // the same order); only the per-pixel fp64 summation grouping differs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "dev_layout.h"
 #include "device_common.h"
@@ -693,6 +694,19 @@ static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
   return hipEventRecord(plan.events[n++], st);
 }
 
+// RTGPU_DEBUG_SYNC (diagnostics): wait for each launch and name the one that
+// failed, so a device fault is attributed to its kernel and bounce.
+#define RTG_LAUNCHED(name, bounce)                                                                      \
+  do {                                                                                                 \
+    if (plan.debug_sync) {                                                                             \
+      const hipError_t de = hipStreamSynchronize(st);                                                  \
+      if (de != hipSuccess) {                                                                          \
+        fprintf(stderr, "rtgpu: %s (bounce %d) failed: %s\n", name, int(bounce), hipGetErrorString(de)); \
+        return de;                                                                                     \
+      }                                                                                                \
+    }                                                                                                  \
+  } while (0)
+
 template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
   const int cus = plan.num_cus;
@@ -729,18 +743,22 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
         gext = gext < max_trav_blocks ? gext : max_trav_blocks;
         hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+        RTG_LAUNCHED("k_extend", b);
         if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+        RTG_LAUNCHED("k_shade", b);
       } else {
         const void* fx = (const void*)k_extend<STACK, kCount, kVol, false, kQuant>;
         int gext = grid_for(fx, 256, 0, nslots, cus);
         gext = gext < max_trav_blocks ? gext : max_trav_blocks;
         hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+        RTG_LAUNCHED("k_extend", b);
         if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
                            cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+        RTG_LAUNCHED("k_shade", b);
       }
       // no lights: k_shade writes no NEE job (sampleLightMIS needs a light,
       // camera.go:502), so the shadow and apply launches are skipped; k_shade
@@ -749,8 +767,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
         if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd), dim3(256), 0, st, sc, a,
                            cnt_shadow, fetch_sh, fetch_ext);
+        RTG_LAUNCHED("k_shadow", b);
         if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap), dim3(256), 0, st, a, cnt_shadow);
+        RTG_LAUNCHED("k_nee_apply", b);
       }
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
         // long-tail scenes (RandomScene depth 50): stop once every path ended
@@ -763,8 +783,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, 
         if (left == 0) break;
       }
     }
-    if (!kCount)
+    if (!kCount) {
       hipLaunchKernelGGL(k_accum, dim3(grid_for((const void*)k_accum, 256, 0, a.npix, cus)), dim3(256), 0, st, a, sb);
+      RTG_LAUNCHED("k_accum", plan.max_depth);
+    }
   }
   return hipGetLastError();
 }

@@ -282,9 +282,14 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *   RT_OPT_NODE_FORMAT: the BVH4 node records the traversal reads:
  *     RT_NODES_FP32 (default) = 128-B nodes, fp32 child boxes rounded
  *     outward from the fp64 boxes; RT_NODES_QUANT8 = 64-B nodes, child
- *     planes as 8-bit steps of a per-node frame, widened by a margin that
- *     covers the slab test's rounding (half the node bytes, looser boxes;
- *     the same closest hits).  Scenes holding a RotateX/RotateZ wrapper
+ *     planes as 8-bit steps of a per-node frame, widened by a margin of
+ *     2^-17 of the node's largest |coordinate| (half the node bytes, looser
+ *     boxes).  The margin covers the slab test's fp32 rounding for ray
+ *     origins up to ~20 node magnitudes from the node (tests/quant_probe.cpp);
+ *     a ray from farther away (a node near its space's origin seen from
+ *     hundreds of magnitudes off) can lose a box at the last ulp, so the
+ *     closest hits equal the fp32 format's only within that envelope (every
+ *     BASELINE scene is inside it).  Scenes holding a RotateX/RotateZ wrapper
  *     always use RT_NODES_FP32 (their node boxes decide which rays reach
  *     an object, transform.go:201-351).                                   */
 /* Schedule options (take effect at the next render; 0 = automatic).  They
