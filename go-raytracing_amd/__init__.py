@@ -29,7 +29,7 @@ ASSET_DIR = os.path.join(REPO_DIR, "assets")
 
 RT_OK = 0
 RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER, RT_OPT_NODE_FORMAT = 1, 2, 3
-RT_OPT_BATCH_SLOTS, RT_OPT_REFILL, RT_OPT_MAX_BLOCKS = 4, 5, 6
+RT_OPT_BATCH_SLOTS, RT_OPT_REFILL, RT_OPT_MAX_BLOCKS, RT_OPT_STREAMS = 4, 5, 6, 7
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
@@ -470,13 +470,15 @@ class Context:
         8-bit child planes with a conservative margin); next upload."""
         self.set_option(RT_OPT_NODE_FORMAT, {"fp32": RT_NODES_FP32, "quant8": RT_NODES_QUANT8}[fmt])
 
-    def set_schedule(self, batch_slots: int = 0, refill: int = 0, max_blocks: int = 0):
+    def set_schedule(self, batch_slots: int = 0, refill: int = 0, max_blocks: int = 0, streams: int = 0):
         """Schedule options (0 = automatic) for the next renders: path slots per
         batch, idle lanes before a wave claims more rays, cap on the persistent
-        traversal grids.  They never change the image."""
+        traversal grids, one or two twin streams.  They never change the image
+        (DESIGN.md §3)."""
         self.set_option(RT_OPT_BATCH_SLOTS, batch_slots)
         self.set_option(RT_OPT_REFILL, refill)
         self.set_option(RT_OPT_MAX_BLOCKS, max_blocks)
+        self.set_option(RT_OPT_STREAMS, streams)
 
     def set_kernel_timing(self, enable: bool = True):
         self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))

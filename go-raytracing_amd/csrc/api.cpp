@@ -68,6 +68,15 @@ struct rt_ctx {
   size_t opt_slots = 0;
   int opt_refill = 0;
   int opt_blocks = 0;
+  int opt_streams = 0;            // RT_OPT_STREAMS: 1 or 2 twins (0 = automatic: 2)
+  // twins of the last render (render_wave): the second's stream, the join
+  // events, and where each twin's hit records and pixels are
+  hipStream_t stream2 = nullptr;
+  hipEvent_t twin_ev0 = nullptr, twin_ev1 = nullptr;
+  int num_twins = 1;
+  const float4* twin_hit[2] = {nullptr, nullptr};
+  const uint32_t* twin_pix[2] = {nullptr, nullptr};
+  uint32_t twin_npix[2] = {0, 0};
   // device BVH build (RT_BLAS_DEVICE) of the last upload
   uint32_t dev_nodes = 0, dev_leaves = 0;   // nodes / leaves added on the device
   double build_ms = 0.0;                    // wall time of the device builds
@@ -240,11 +249,27 @@ int check_render_error(rt_ctx* ctx, bool wait) {
 // batches sized to keep ~4M paths in flight.
 int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const std::vector<int4>& tiles, float* d_out,
                 hipStream_t st, bool count, unsigned long long* host_counters, double* ms) {
+  // Twins (wavefront.hip run_batches): tiles dealt alternately to two halves
+  // of the pixel list, each rendered on its own stream so one half's kernel
+  // tails overlap the other half's next kernel.  RT_OPT_STREAMS = 1 keeps one.
+  static const int env_twins = [] {
+    const char* e = getenv("RTGPU_STREAMS");
+    return e ? std::min(2, std::max(1, atoi(e))) : 0;
+  }();
+  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : 2;
+  const int nt = (want_twins >= 2 && tiles.size() >= 2) ? 2 : 1;
   std::vector<uint32_t>& px = ctx->pix_host;
   px.clear();
-  for (const int4& t : tiles)
-    for (int y = t.y; y < t.y + t.w; ++y)
-      for (int x = t.x; x < t.x + t.z; ++x) px.push_back(uint32_t(y) * uint32_t(dc.width) + uint32_t(x));
+  uint32_t twin_npix[2] = {0, 0};
+  for (int t = 0; t < nt; ++t) {
+    const size_t before = px.size();
+    for (size_t k = size_t(t); k < tiles.size(); k += size_t(nt)) {
+      const int4& tl = tiles[k];
+      for (int y = tl.y; y < tl.y + tl.w; ++y)
+        for (int x = tl.x; x < tl.x + tl.z; ++x) px.push_back(uint32_t(y) * uint32_t(dc.width) + uint32_t(x));
+    }
+    twin_npix[t] = uint32_t(px.size() - before);
+  }
   const uint32_t npix = uint32_t(px.size());
   const uint32_t spp = uint32_t(p->samples_per_pixel);
   // Path slots per batch: as many as fit in half the free HBM, up to 512M
@@ -269,14 +294,14 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   const uint32_t max_spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
   const uint32_t nbatch = (spp + max_spb - 1) / max_spb;
   const uint32_t spb = (spp + nbatch - 1) / nbatch;
-  const size_t nslots = size_t(spb) * npix;
+  const size_t nslots = size_t(spb) * npix;   // over both twins
   int rc;
   if (ctx->wslots < nslots) {
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
     ctx->wslots = 0;
     if ((rc = ensure(ctx, ctx->wstate, nslots * size_t(kSlotF4) * sizeof(float4)))) return rc;
-    if ((rc = ensure(ctx, ctx->wq, nslots * 2 * sizeof(uint32_t) + CNT_WORDS_Q * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(ctx, ctx->wq, nslots * 2 * sizeof(uint32_t) + 2 * CNT_WORDS_Q * sizeof(uint32_t)))) return rc;
     ctx->wslots = nslots;
   }
   if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
@@ -299,52 +324,87 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
 #else
   if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
 #endif
-  WaveArgs a{};
-  float4* base = static_cast<float4*>(ctx->wstate.p);
-  const size_t S = ctx->wslots;
-  for (int k = 0; k < 2; ++k) {
-    float4* sb = base + size_t(3 * k) * S;
-    a.s[k] = PathStream{sb, sb + S, sb + 2 * S};
-  }
-  a.hit = base + 6 * S; a.Lout = base + 7 * S;
-  a.sj_p = base + 8 * S; a.sj_a = base + 9 * S; a.sj_h = base + 10 * S;
-  a.ne_a = base + 11 * S; a.ne_h = base + 12 * S; a.ne_beta = base + 13 * S;
-  uint32_t* qb = static_cast<uint32_t*>(ctx->wq.p);
-  a.counts = qb;
-  a.sj_info = qb + CNT_WORDS_Q;
-  a.sj_vis = a.sj_info + S;
-  a.pixels = static_cast<const uint32_t*>(ctx->wpix.p);
-  a.npix = npix;
-  a.acc = static_cast<double*>(ctx->wacc.p);
-  a.seed = p->seed;
-  a.max_depth = p->max_depth;
-  a.counters = static_cast<unsigned long long*>(ctx->counters.p);
-  a.err = static_cast<int*>(ctx->errflag.p);
   // lanes that must want an item before a wave claims a new run (pool_take):
   // within [1, 64] (the wave size), or no wave would ever claim
   static const int refill = [] {
     const char* e = getenv("RTGPU_REFILL");
     return e ? std::min(64, std::max(1, atoi(e))) : 16;
   }();
-  a.refill = ctx->opt_refill ? ctx->opt_refill : refill;
-  WavePlan plan{};
-  plan.max_blocks = ctx->opt_blocks;
-  static const int debug_sync = [] {
-    const char* e = getenv("RTGPU_DEBUG_SYNC");
-    return e && atoi(e) > 0 ? 1 : 0;
+  // LDS stack ring (8 entries per lane by default, 16 with RTGPU_STACK=16) +
+  // global spill up to kStackMax: scenes of any supported depth run with the
+  // small ring.
+  static const int lds_stack = [] {
+    const char* e = getenv("RTGPU_STACK");
+#ifdef RTG_RING24
+    if (e && atoi(e) == 24) return 24;   // diagnostic build only (DESIGN §7)
+#endif
+    return e && atoi(e) == 16 ? 16 : 8;
   }();
-  plan.debug_sync = debug_sync;
+  const int stack = lds_stack;
+  const uint32_t spill_lanes = uint32_t(std::max(1, ctx->num_cus)) * kSpillLanesPerCU;
+  const int spill_cap = kStackMax - stack;
+  const size_t spill_words = size_t(spill_lanes) * size_t(spill_cap);   // one twin's spill area
+  if ((rc = ensure(ctx, ctx->wspill, size_t(nt) * spill_words * sizeof(uint32_t)))) return rc;
+  // each twin: kSlotF4 arrays of its own S_t slots, its queue counters and
+  // job words, its slice of the pixel list and the fp64 sums, its spill area
+  WaveArgs as[2]{};
+  hipStream_t sts[2] = {st, ctx->stream2};
+  float4* fbase = static_cast<float4*>(ctx->wstate.p);
+  uint32_t* qbase = static_cast<uint32_t*>(ctx->wq.p);
+  uint32_t pix_off = 0;
+  for (int t = 0; t < nt; ++t) {
+    WaveArgs& a = as[t];
+    const size_t S = size_t(spb) * twin_npix[t];
+    for (int k = 0; k < 2; ++k) {
+      float4* sb = fbase + size_t(3 * k) * S;
+      a.s[k] = PathStream{sb, sb + S, sb + 2 * S};
+    }
+    a.hit = fbase + 6 * S; a.Lout = fbase + 7 * S;
+    a.sj_p = fbase + 8 * S; a.sj_a = fbase + 9 * S; a.sj_h = fbase + 10 * S;
+    a.ne_a = fbase + 11 * S; a.ne_h = fbase + 12 * S; a.ne_beta = fbase + 13 * S;
+    fbase += size_t(kSlotF4) * S;
+    a.counts = qbase;
+    a.sj_info = qbase + CNT_WORDS_Q;
+    a.sj_vis = a.sj_info + S;
+    qbase += CNT_WORDS_Q + 2 * S;
+    a.pixels = static_cast<const uint32_t*>(ctx->wpix.p) + pix_off;
+    a.npix = twin_npix[t];
+    a.acc = static_cast<double*>(ctx->wacc.p) + size_t(pix_off) * 3;
+    pix_off += twin_npix[t];
+    a.seed = p->seed;
+    a.max_depth = p->max_depth;
+    a.counters = static_cast<unsigned long long*>(ctx->counters.p);
+    a.err = static_cast<int*>(ctx->errflag.p);
+    a.refill = ctx->opt_refill ? ctx->opt_refill : refill;
+    a.spill_lanes = spill_lanes;
+    a.spill_cap = spill_cap;
+    a.spill = static_cast<uint32_t*>(ctx->wspill.p) + size_t(t) * spill_words;
+    a.slots = uint32_t(S);
+    ctx->twin_hit[t] = a.hit;
+    ctx->twin_pix[t] = a.pixels;
+    ctx->twin_npix[t] = a.npix;
+  }
+  ctx->num_twins = nt;
+  WavePlan plan{};
   plan.spp = spp;
   plan.samples_per_batch = spb;
   plan.sample_offset = uint32_t(p->sample_offset);
   plan.max_depth = p->max_depth;
   plan.num_cus = ctx->num_cus;
+  plan.max_blocks = ctx->opt_blocks;
+  plan.num_twins = nt;
+  static const int debug_sync = [] {
+    const char* e = getenv("RTGPU_DEBUG_SYNC");
+    return e && atoi(e) > 0 ? 1 : 0;
+  }();
+  plan.debug_sync = debug_sync;
   plan.probe_host = ctx->probe_pinned;
   ctx->tev_used = 0;
   if (ctx->timing) {
-    // worst case: 4 events per bounce per batch
+    // worst case: 2 events per timed launch, 3 timed launches per bounce, per batch and twin
     const size_t batches = (spp + spb - 1) / spb;
-    const size_t want = std::min<size_t>(MAX_TIMING_EVENTS, batches * size_t(std::max(1, p->max_depth)) * 4 + 4);
+    const size_t want = std::min<size_t>(MAX_TIMING_EVENTS,
+                                         batches * size_t(std::max(1, p->max_depth)) * 6 * size_t(nt) + 4);
     while (ctx->tev.size() < want) {
       hipEvent_t e = nullptr;
       HIPCHK(hipEventCreate(&e));
@@ -356,25 +416,17 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     plan.max_events = int(ctx->tev.size());
     plan.num_events = &ctx->tev_used;
   }
-  // LDS stack ring (8 entries per lane by default, 16 with RTGPU_STACK=16) +
-  // global spill
-  // up to kStackMax: scenes of any supported depth run with the small ring.
-  static const int lds_stack = [] {
-    const char* e = getenv("RTGPU_STACK");
-#ifdef RTG_RING24
-    if (e && atoi(e) == 24) return 24;   // diagnostic build only (DESIGN §7)
-#endif
-    return e && atoi(e) == 16 ? 16 : 8;
-  }();
-  const int stack = lds_stack;
-  a.spill_lanes = uint32_t(std::max(1, ctx->num_cus)) * kSpillLanesPerCU;
-  a.spill_cap = kStackMax - stack;
-  if ((rc = ensure(ctx, ctx->wspill, size_t(a.spill_lanes) * size_t(a.spill_cap) * sizeof(uint32_t)))) return rc;
-  a.spill = static_cast<uint32_t*>(ctx->wspill.p);
-  a.slots = uint32_t(S);
   if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(hipEventRecord(ctx->kev0, st));
-  HIPCHK(launch_wavefront(ctx->dscene, dc, a, plan, stack, count, d_out, p->accumulate ? 1 : 0, st));
+  if (nt > 1) {   // the second twin's stream starts after the caller's stream reached here
+    HIPCHK(hipEventRecord(ctx->twin_ev0, st));
+    HIPCHK(hipStreamWaitEvent(ctx->stream2, ctx->twin_ev0, 0));
+  }
+  HIPCHK(launch_wavefront(ctx->dscene, dc, as, sts, plan, stack, count, d_out, p->accumulate ? 1 : 0));
+  if (nt > 1) {   // ... and the caller's stream continues once it has finished
+    HIPCHK(hipEventRecord(ctx->twin_ev1, ctx->stream2));
+    HIPCHK(hipStreamWaitEvent(st, ctx->twin_ev1, 0));
+  }
   HIPCHK(hipEventRecord(ctx->kev1, st));
   ctx->kev_recorded = true;
   if (ms) HIPCHK(hipEventRecord(ctx->ev1, st));
@@ -520,6 +572,9 @@ int rt_ctx_create(int device, rt_ctx** out) {
       hipEventCreateWithFlags(&ctx->pix_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&ctx->probe_pinned), 64) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->fan_ev, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->twin_ev0, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->twin_ev1, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess ||
       hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
     delete ctx;
@@ -591,6 +646,9 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
   if (ctx->fan_ev) (void)hipEventDestroy(ctx->fan_ev);
+  if (ctx->twin_ev0) (void)hipEventDestroy(ctx->twin_ev0);
+  if (ctx->twin_ev1) (void)hipEventDestroy(ctx->twin_ev1);
+  if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
   if (ctx->join_ev) (void)hipEventDestroy(ctx->join_ev);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -628,6 +686,11 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (key == RT_OPT_REFILL) {
     if (value < 0 || value > 64) return set_err(ctx, RT_ERR_INVALID, "refill must be 0 (default) or 1..64");
     ctx->opt_refill = value;
+    return RT_OK;
+  }
+  if (key == RT_OPT_STREAMS) {
+    if (value < 0 || value > 2) return set_err(ctx, RT_ERR_INVALID, "streams must be 0 (default), 1 or 2");
+    ctx->opt_streams = value;
     return RT_OK;
   }
   if (key == RT_OPT_MAX_BLOCKS) {
@@ -959,10 +1022,10 @@ int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out) {
   HIPCHK(hipSetDevice(ctx->device));
   std::memset(out, 0, sizeof(*out));
   if (ctx->tev_used == 0) return set_err(ctx, RT_ERR_INVALID, "no timed render recorded (rt_set_kernel_timing)");
-  HIPCHK(hipEventSynchronize(ctx->tev[ctx->tev_used - 1]));
+  HIPCHK(hipEventSynchronize(ctx->kev1));   // after both twins' streams joined
   double* ms[3] = {&out->extend_ms, &out->shade_ms, &out->shadow_ms};
   int32_t* nl[3] = {&out->extend_launches, &out->shade_launches, &out->shadow_launches};
-  for (int i = 0; i + 1 < ctx->tev_used; ++i) {
+  for (int i = 0; i + 1 < ctx->tev_used; i += 2) {   // (begin, end) per launch
     const int c = ctx->tev_class[i];
     if (c > KC_SHADOW) continue;
     float f = 0.f;
@@ -1033,9 +1096,8 @@ int rt_extend_first_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, 
   int32_t* top = static_cast<int32_t*>(ctx->probe.p);
   int32_t* prim = top + n;
   float* t = reinterpret_cast<float*>(prim + n);
-  const float4* hit = static_cast<const float4*>(ctx->wstate.p) + 6 * ctx->wslots;   // WaveArgs::hit (render_wave)
-  HIPCHK(launch_hit_ids(ctx->dscene, hit, static_cast<const uint32_t*>(ctx->wpix.p), uint32_t(ctx->pix_host.size()),
-                        top, prim, t, ctx->stream));
+  for (int k = 0; k < ctx->num_twins; ++k)   // each twin's hit records (render_wave)
+    HIPCHK(launch_hit_ids(ctx->dscene, ctx->twin_hit[k], ctx->twin_pix[k], ctx->twin_npix[k], top, prim, t, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -69,10 +69,11 @@ struct WavePlan {
   int32_t num_cus;
   int32_t max_blocks;       // > 0: cap on the persistent traversal grids (RT_OPT_MAX_BLOCKS)
   int32_t debug_sync;       // RTGPU_DEBUG_SYNC=1: synchronise after every launch, name a failing kernel
-  uint32_t* probe_host;     // pinned word for the long-tail early exit
-  // Per-launch timing (rt_set_kernel_timing): an event is recorded before
-  // every extend/shade/shadow launch and after every shadow launch;
-  // ev_class[i] names the kernel running between events i and i+1.
+  int32_t num_twins;        // 1 or 2 halves of the pixel list on their own streams (run_batches)
+  uint32_t* probe_host;     // pinned words (one per twin) for the long-tail early exit
+  // Per-launch timing (rt_set_kernel_timing): events 2k and 2k+1 are
+  // recorded before and after one extend / shade / shadow launch on its
+  // stream; ev_class[2k] names the kernel.
   hipEvent_t* events;       // nullptr: timing off
   uint8_t* ev_class;
   int max_events;
@@ -83,7 +84,8 @@ enum : uint8_t { KC_EXTEND = 0, KC_SHADE = 1, KC_SHADOW = 2, KC_OTHER = 3 };
 // Counter blocks (16 x u64 each): one per kernel class.
 constexpr int CNT_BLOCK = 24;
 
-hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs& a, const WavePlan& plan, int stack,
-                            bool count, float* out, int accumulate, hipStream_t st);
+// as[t] / sts[t] for t < plan.num_twins: each twin's buffers and stream.
+hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
+                            const WavePlan& plan, int stack, bool count, float* out, int accumulate);
 
 }  // namespace rtg

@@ -685,18 +685,27 @@ static int grid_for(const void* fn, int block, size_t lds, uint32_t items, int c
   return int(need < resident ? need : resident);
 }
 
-// Record the next timing event; the interval it opens belongs to `cls`.
-static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
+// Per-launch timing: one event before and one after each timed launch, on
+// the launch's stream (so a launch's interval is its own even when the twin
+// streams' kernels overlap).
+static hipError_t mark_begin(const WavePlan& plan, uint8_t cls, hipStream_t st) {
   if (!plan.events) return hipSuccess;
   int& n = *plan.num_events;
-  if (n >= plan.max_events) return hipSuccess;   // pool exhausted: later launches untimed
+  if (n + 2 > plan.max_events) return hipSuccess;   // pool exhausted: later launches untimed
   plan.ev_class[n] = cls;
+  plan.ev_class[n + 1] = KC_OTHER;
+  return hipEventRecord(plan.events[n++], st);
+}
+static hipError_t mark_end(const WavePlan& plan, hipStream_t st) {
+  if (!plan.events) return hipSuccess;
+  int& n = *plan.num_events;
+  if (n == 0 || (n & 1) == 0) return hipSuccess;   // its begin was not recorded
   return hipEventRecord(plan.events[n++], st);
 }
 
 // RTGPU_DEBUG_SYNC (diagnostics): wait for each launch and name the one that
 // failed, so a device fault is attributed to its kernel and bounce.
-#define RTG_LAUNCHED(name, bounce)                                                                      \
+#define RTG_LAUNCHED(name, bounce, st)                                                                  \
   do {                                                                                                 \
     if (plan.debug_sync) {                                                                             \
       const hipError_t de = hipStreamSynchronize(st);                                                  \
@@ -707,105 +716,131 @@ static hipError_t mark(const WavePlan& plan, uint8_t cls, hipStream_t st) {
     }                                                                                                  \
   } while (0)
 
+// The render's work is split into twins (WavePlan::num_twins, 1 or 2):
+// disjoint halves of the pixel list, each with its own path slots, queue
+// counters, spill area and HIP stream, enqueued bounce by bounce in
+// alternation.  A persistent kernel ends with a tail in which only the
+// waves holding the last, longest rays still run (about 0.4 ms per launch
+// on CornellBoxLucy, a fixed cost per launch); the other twin's next
+// kernel is already queued on its own stream and its workgroups take the
+// compute units those waves free, so the tails overlap with work.  Each
+// pixel belongs to one twin and keeps its sample order: the frame is
+// bit-identical to a one-stream render.
 template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
-static hipError_t run_batches(const DScene& sc, const DCamera& cam, WaveArgs a, const WavePlan& plan, hipStream_t st) {
+static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
+                              const WavePlan& plan) {
   const int cus = plan.num_cus;
+  const int nt = plan.num_twins;
   const bool nee = sc.num_lights > 0;
   hipError_t e;
-  uint32_t* const cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
-  uint32_t* const cnt_shadow = a.counts + CNT_SHADOW;
-  uint32_t* const fetch_ext = a.counts + CNT_FETCH_EXT;
-  uint32_t* const fetch_sh = a.counts + CNT_FETCH_SH;
   for (uint32_t s0 = 0; s0 < plan.spp; s0 += plan.samples_per_batch) {
     const uint32_t sb = plan.spp - s0 < plan.samples_per_batch ? plan.spp - s0 : plan.samples_per_batch;
-    const uint32_t nslots = sb * a.npix;
     const uint32_t sample_base = plan.sample_offset + s0;
-    hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, a.counts, nslots);
-    if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
-    // one spill column per resident lane; RT_OPT_MAX_BLOCKS may cap it further
-    int max_trav_blocks = int(a.spill_lanes / 256u);
-    if (plan.max_blocks > 0 && plan.max_blocks < max_trav_blocks) max_trav_blocks = plan.max_blocks;
-    const int gsh = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, 0, nslots, cus);
-    int gsd = grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus);
-    gsd = gsd < max_trav_blocks ? gsd : max_trav_blocks;
-    const int gap = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
+    int gext0[2], gext[2], gsh[2], gsd[2], gap[2];
+    for (int t = 0; t < nt; ++t) {
+      const WaveArgs& a = as[t];
+      const hipStream_t st = sts[t];
+      const uint32_t nslots = sb * a.npix;
+      hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, a.counts, nslots);
+      if (kCount) hipLaunchKernelGGL(k_count_samples, dim3(1), dim3(1), 0, st, a, nslots);
+      // one spill column per resident lane; RT_OPT_MAX_BLOCKS may cap it further
+      int max_trav_blocks = int(a.spill_lanes / 256u);
+      if (plan.max_blocks > 0 && plan.max_blocks < max_trav_blocks) max_trav_blocks = plan.max_blocks;
+      auto cap = [&](int g) { return g < max_trav_blocks ? g : max_trav_blocks; };
+      gsh[t] = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, 0, nslots, cus);
+      gsd[t] = cap(grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus));
+      gap[t] = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
+      gext0[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, true, kQuant>, 256, 0, nslots, cus));
+      gext[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, false, kQuant>, 256, 0, nslots, cus));
+    }
     for (int b = 0; b < plan.max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
+      for (int t = 0; t < nt; ++t) {
+        const WaveArgs& a = as[t];
+        const hipStream_t st = sts[t];
+        uint32_t* const cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
+        uint32_t* const cnt_shadow = a.counts + CNT_SHADOW;
+        uint32_t* const fetch_ext = a.counts + CNT_FETCH_EXT;
+        uint32_t* const fetch_sh = a.counts + CNT_FETCH_SH;
 #ifdef RTG_GUARD
-      // poison the hit records: k_shade reports any that k_extend did not write
-      if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
+        // poison the hit records: k_shade reports any that k_extend did not write
+        if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
 #endif
-      if ((e = mark(plan, KC_EXTEND, st)) != hipSuccess) return e;
-      // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
-      if (b == 0) {
-        const void* fx = (const void*)k_extend<STACK, kCount, kVol, true, kQuant>;
-        int gext = grid_for(fx, 256, 0, nslots, cus);
-        gext = gext < max_trav_blocks ? gext : max_trav_blocks;
-        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
-                           cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
-        RTG_LAUNCHED("k_extend", b);
-        if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
-                           cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
-        RTG_LAUNCHED("k_shade", b);
-      } else {
-        const void* fx = (const void*)k_extend<STACK, kCount, kVol, false, kQuant>;
-        int gext = grid_for(fx, 256, 0, nslots, cus);
-        gext = gext < max_trav_blocks ? gext : max_trav_blocks;
-        hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant>), dim3(gext), dim3(256), 0, st, sc, cam, a, a.s[c],
-                           cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
-        RTG_LAUNCHED("k_extend", b);
-        if ((e = mark(plan, KC_SHADE, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh), dim3(256), 0, st, sc, cam, a, a.s[c],
-                           cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
-        RTG_LAUNCHED("k_shade", b);
-      }
-      // no lights: k_shade writes no NEE job (sampleLightMIS needs a light,
-      // camera.go:502), so the shadow and apply launches are skipped; k_shade
-      // then resets the next extend's fetch counter itself
-      if (nee) {
-        if ((e = mark(plan, KC_SHADOW, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd), dim3(256), 0, st, sc, a,
-                           cnt_shadow, fetch_sh, fetch_ext);
-        RTG_LAUNCHED("k_shadow", b);
-        if ((e = mark(plan, KC_OTHER, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap), dim3(256), 0, st, a, cnt_shadow);
-        RTG_LAUNCHED("k_nee_apply", b);
+        // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
+        if ((e = mark_begin(plan, KC_EXTEND, st)) != hipSuccess) return e;
+        if (b == 0)
+          hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
+                             a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+        else
+          hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant>), dim3(gext[t]), dim3(256), 0, st, sc, cam, a,
+                             a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+        if ((e = mark_end(plan, st)) != hipSuccess) return e;
+        RTG_LAUNCHED("k_extend", b, st);
+        if ((e = mark_begin(plan, KC_SHADE, st)) != hipSuccess) return e;
+        if (b == 0)
+          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh[t]), dim3(256), 0, st, sc, cam, a, a.s[c],
+                             cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+        else
+          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh[t]), dim3(256), 0, st, sc, cam, a, a.s[c],
+                             cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+        if ((e = mark_end(plan, st)) != hipSuccess) return e;
+        RTG_LAUNCHED("k_shade", b, st);
+        // no lights: k_shade writes no NEE job (sampleLightMIS needs a light,
+        // camera.go:502), so the shadow and apply launches are skipped; k_shade
+        // then resets the next extend's fetch counter itself
+        if (nee) {
+          if ((e = mark_begin(plan, KC_SHADOW, st)) != hipSuccess) return e;
+          hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd[t]), dim3(256), 0, st, sc, a,
+                             cnt_shadow, fetch_sh, fetch_ext);
+          if ((e = mark_end(plan, st)) != hipSuccess) return e;
+          RTG_LAUNCHED("k_shadow", b, st);
+          hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap[t]), dim3(256), 0, st, a, cnt_shadow);
+          RTG_LAUNCHED("k_nee_apply", b, st);
+        }
       }
       if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
-        // long-tail scenes (RandomScene depth 50): stop once every path ended
+        // long-tail scenes (RandomScene depth 50): stop once every path of
+        // every twin ended
+        for (int t = 0; t < nt; ++t)
+          if ((e = hipMemcpyAsync(plan.probe_host + t, as[t].counts + (nx ? CNT_STREAM1 : CNT_STREAM0), sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, sts[t])) != hipSuccess)
+            return e;
         uint32_t left = 0;
-        if ((e = hipMemcpyAsync(plan.probe_host, cnt_stream[nx], sizeof(uint32_t), hipMemcpyDeviceToHost, st)) !=
-            hipSuccess)
-          return e;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        left = *plan.probe_host;
+        for (int t = 0; t < nt; ++t) {
+          if ((e = hipStreamSynchronize(sts[t])) != hipSuccess) return e;
+          left += plan.probe_host[t];
+        }
         if (left == 0) break;
       }
     }
-    if (!kCount) {
-      hipLaunchKernelGGL(k_accum, dim3(grid_for((const void*)k_accum, 256, 0, a.npix, cus)), dim3(256), 0, st, a, sb);
-      RTG_LAUNCHED("k_accum", plan.max_depth);
-    }
+    if (!kCount)
+      for (int t = 0; t < nt; ++t) {
+        const hipStream_t st = sts[t];
+        hipLaunchKernelGGL(k_accum, dim3(grid_for((const void*)k_accum, 256, 0, as[t].npix, cus)), dim3(256), 0, st,
+                           as[t], sb);
+        RTG_LAUNCHED("k_accum", plan.max_depth, st);
+      }
   }
   return hipGetLastError();
 }
 
-hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs& a, const WavePlan& plan, int stack,
-                            bool count, float* out, int accumulate, hipStream_t st) {
+hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
+                            const WavePlan& plan, int stack, bool count, float* out, int accumulate) {
   hipError_t e;
-  if ((e = hipMemsetAsync(a.acc, 0, size_t(a.npix) * 3 * sizeof(double), st)) != hipSuccess) return e;
+  const int nt = plan.num_twins;
+  for (int t = 0; t < nt; ++t)
+    if ((e = hipMemsetAsync(as[t].acc, 0, size_t(as[t].npix) * 3 * sizeof(double), sts[t])) != hipSuccess) return e;
   if (plan.max_depth > 0) {
     // the kVol variants also carry the rare primitives (circles)
     const bool vol = sc.has_volumes != 0 || sc.n_circles > 0;
 #define RUN2(S, C, V, Q)                                                           \
   do {                                                                             \
     if (envis) {                                                                   \
-      if (fancy) e = run_batches<S, C, V, true, true, Q>(sc, cam, a, plan, st);    \
-      else e = run_batches<S, C, V, true, false, Q>(sc, cam, a, plan, st);         \
+      if (fancy) e = run_batches<S, C, V, true, true, Q>(sc, cam, as, sts, plan);  \
+      else e = run_batches<S, C, V, true, false, Q>(sc, cam, as, sts, plan);       \
     } else {                                                                       \
-      if (fancy) e = run_batches<S, C, V, false, true, Q>(sc, cam, a, plan, st);   \
-      else e = run_batches<S, C, V, false, false, Q>(sc, cam, a, plan, st);        \
+      if (fancy) e = run_batches<S, C, V, false, true, Q>(sc, cam, as, sts, plan); \
+      else e = run_batches<S, C, V, false, false, Q>(sc, cam, as, sts, plan);      \
     }                                                                              \
   } while (0)
     // RT_NODES_QUANT8 scenes run the quantised-node traversal (its own kernels:
@@ -841,8 +876,9 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     if (e != hipSuccess) return e;
   }
   if (!count)
-    hipLaunchKernelGGL(k_finalize, dim3(grid_for((const void*)k_finalize, 256, 0, a.npix, plan.num_cus)), dim3(256), 0,
-                       st, a, out, accumulate);
+    for (int t = 0; t < nt; ++t)
+      hipLaunchKernelGGL(k_finalize, dim3(grid_for((const void*)k_finalize, 256, 0, as[t].npix, plan.num_cus)),
+                         dim3(256), 0, sts[t], as[t], out, accumulate);
   return hipGetLastError();
 }
 #endif  // RTG_HOST_EMU

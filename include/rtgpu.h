@@ -299,9 +299,12 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *     HBM, at most 512M).
  *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
  *     of rays (default 16).
- *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups). */
+ *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups).
+ *   RT_OPT_STREAMS: 2 (default) renders the bucket tiles as two halves on
+ *     two HIP streams whose kernels overlap each other's tails; 1 keeps one
+ *     stream.                                                              */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
-       RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6 };
+       RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);

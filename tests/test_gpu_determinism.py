@@ -32,10 +32,11 @@ def lucy(g):
 
 
 def _schedules(npix):
-    # (batch slots, refill, max persistent blocks): automatic; three batches
-    # per frame with waves that claim only when every lane idles on a small
-    # grid; many small batches claiming as soon as one lane idles
-    return [(0, 0, 0), (npix * 6, 64, 37), (npix * 2, 1, 600)]
+    # (batch slots, refill, max persistent blocks, streams): automatic (two
+    # twin streams); three batches per frame with waves that claim only when
+    # every lane idles on a small grid, one stream; many small batches
+    # claiming as soon as one lane idles, two streams
+    return [(0, 0, 0, 0), (npix * 6, 64, 37, 1), (npix * 2, 1, 600, 2)]
 
 
 def test_c4_full_mesh_schedule_independent(g, O, lucy):
@@ -47,8 +48,8 @@ def test_c4_full_mesh_schedule_independent(g, O, lucy):
         assert c.info().triangles >= 280000
         p = g.make_params(SPP, cam.max_depth, seed=SEED)
         frames, hits = [], []
-        for slots, refill, blocks in _schedules(npix):
-            c.set_schedule(slots, refill, blocks)
+        for slots, refill, blocks, streams in _schedules(npix):
+            c.set_schedule(slots, refill, blocks, streams)
             f, _ = c.render(cam, p)
             frames.append(f)
             hits.append([c.extend_first_hits(cam, SEED, k) for k in (0, 7)])
@@ -87,8 +88,8 @@ def test_other_configs_schedule_independent(g, name, kw):
         c.upload(s.desc)
         p = g.make_params(8, cam.max_depth, seed=SEED)
         frames = []
-        for slots, refill, blocks in _schedules(npix):
-            c.set_schedule(slots, refill, blocks)
+        for slots, refill, blocks, streams in _schedules(npix):
+            c.set_schedule(slots, refill, blocks, streams)
             frames.append(c.render(cam, p)[0])
         for k in range(1, len(frames)):
             assert np.array_equal(frames[0], frames[k]), f"{name}: schedule {k} frame differs"
@@ -101,4 +102,6 @@ def test_schedule_option_validation(g, ctx):
         ctx.set_option(g.RT_OPT_REFILL, 65)
     with pytest.raises(g.RTError):
         ctx.set_option(g.RT_OPT_BATCH_SLOTS, -1)
-    ctx.set_schedule(0, 0, 0)
+    with pytest.raises(g.RTError):
+        ctx.set_option(g.RT_OPT_STREAMS, 3)
+    ctx.set_schedule(0, 0, 0, 0)
