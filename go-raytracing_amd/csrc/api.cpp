@@ -452,6 +452,13 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     }
   }
 #endif
+#ifdef RTG_GUARD
+  {   // diagnostic build: report the first out-of-range index of this render
+    unsigned int gr[4] = {0, 0, 0, 0};
+    HIPCHK(guard_report(gr));
+    if (gr[0]) fprintf(stderr, "RTG_GUARD: %u bad indices, first at site %u: index %u >= length %u\n", gr[0], gr[1], gr[2], gr[3]);
+  }
+#endif
   if (count || ms) {
     if ((rc = check_render_error(ctx, true))) return rc;
     if (ms) {

@@ -21,14 +21,24 @@
 namespace rtg {
 
 // RTG_GUARD (diagnostic build only, never the product): every device array
-// index is checked against its length; a bad index is reported once per
-// site class by printf and clamped, so a bad index shows up as a message
-// instead of a memory fault.
+// index is checked against its length; a bad index is clamped and counted,
+// and the first one's site / index / length are kept in rtg_guard_rec for
+// the host (rtg_guard_report after each render).  No device printf: its
+// hostcall requests aborted the runtime ("Hostcall: invalid service request")
+// inside these persistent kernels, which is what made round 2's guard builds
+// fault and drift.
 #ifdef RTG_GUARD
-__device__ int rtg_guard_hits;
+__device__ unsigned int rtg_guard_rec[4];   // count, site, index, length of the first bad index
+__device__ __forceinline__ void rtg_guard_note(int site, uint32_t i, uint32_t n) {
+  if (atomicAdd(&rtg_guard_rec[0], 1u) == 0u) {
+    rtg_guard_rec[1] = uint32_t(site);
+    rtg_guard_rec[2] = i;
+    rtg_guard_rec[3] = n;
+  }
+}
 __device__ __forceinline__ uint32_t rtg_gix(uint32_t i, uint32_t n, int site) {
   if (i >= n) {
-    if (atomicAdd(&rtg_guard_hits, 1) < 16) printf("RTG_GUARD site %d: index %u >= %u\n", site, i, n);
+    rtg_guard_note(site, i, n);
     return n ? n - 1u : 0u;
   }
   return i;

@@ -491,23 +491,99 @@ struct Flattener {
   // contain the objects Hit actually sees: RotateX/RotateZ rotate their bbox
   // by +theta but the ray by +theta too (transform.go:201-268), so the
   // effective object lies outside its bbox and is never culled here.
-  DRefBox instance_cull_box(const rt_hittable& h, int inst) {
+  DRefBox instance_cull_box(int g, const rt_hittable& h, int inst) {
     const DInstance& in = S.instances[inst];
     for (int k = 0; k < in.nwrap; ++k)
       if (in.kind[k] == W_ROT_X || in.kind[k] == W_ROT_Z) return infinite_ref_box();
+    double lo[3], hi[3];
+    if (!instance_box(g, lo, hi)) return infinite_ref_box();
     double ext = 0.0;
-    for (int a = 0; a < 3; ++a) {
-      const double lo = h.bbox[2 * a], hi = h.bbox[2 * a + 1];
-      if (!(lo <= hi) || !std::isfinite(lo) || !std::isfinite(hi)) return infinite_ref_box();
-      ext = std::max(ext, std::max(hi - lo, std::max(std::fabs(lo), std::fabs(hi))));
-    }
+    for (int a = 0; a < 3; ++a) ext = std::max(ext, std::max(hi[a] - lo[a], std::max(std::fabs(lo[a]), std::fabs(hi[a]))));
     const double pad = 1e-5 * ext + 1e-6;
     DRefBox b{};
     for (int a = 0; a < 3; ++a) {
-      b.lo[a] = round_down(h.bbox[2 * a] - pad);
-      b.hi[a] = round_up(h.bbox[2 * a + 1] + pad);
+      b.lo[a] = round_down(lo[a] - pad);
+      b.hi[a] = round_up(hi[a] + pad);
     }
     return b;
+  }
+
+  // World-space box of a transformed object (a Translate / RotateY / Scale
+  // chain over a BLAS): the wrapper's own bbox (transform.go: the child's box
+  // mapped corner by corner, loose for a rotated object) intersected with the
+  // tight box of the object's geometry mapped to world space (triangle
+  // vertices; other primitives' bbox corners), fp64.  Both contain every
+  // primitive, so culling on it never changes a hit; the tight one lets far
+  // fewer rays enter a rotated mesh instance.  False: no finite box.
+  std::map<int, std::vector<double>> inner_points;   // object-space points per BLAS root graph node
+  bool object_points(int g, std::vector<double>& pts, int depth = 0) {
+    if (!valid_index(g) || depth > 200) return false;
+    const rt_hittable& h = H(g);
+    if (h.kind == RT_TRIANGLE) {
+      pts.insert(pts.end(), h.p, h.p + 9);
+      return true;
+    }
+    if (is_prim(h.kind)) {
+      for (int c = 0; c < 8; ++c)
+        for (int a = 0; a < 3; ++a) pts.push_back(h.bbox[2 * a + ((c >> a) & 1)]);
+      return true;
+    }
+    if (h.kind == RT_BVH_NODE) return object_points(h.a, pts, depth + 1) && (h.a == h.b || object_points(h.b, pts, depth + 1));
+    if (h.kind == RT_LIST || h.kind == RT_BVH_LEAF) {
+      if (!child_range(h)) return false;
+      for (int c : children_of(h))
+        if (!object_points(c, pts, depth + 1)) return false;
+      return true;
+    }
+    return false;
+  }
+  bool instance_box(int g, double lo[3], double hi[3]) {
+    const rt_hittable& top = H(g);
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = top.bbox[2 * a];
+      hi[a] = top.bbox[2 * a + 1];
+      if (!(lo[a] <= hi[a]) || !std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
+    }
+    std::vector<int> chain;   // outermost first
+    int cur = g;
+    while (valid_index(cur) && is_wrapper(H(cur).kind)) {
+      const int k = H(cur).kind;
+      if (k == RT_ROTATE_X || k == RT_ROTATE_Z) return true;   // (never culled anyway)
+      chain.push_back(cur);
+      cur = H(cur).a;
+    }
+    auto it = inner_points.find(cur);
+    if (it == inner_points.end()) {
+      std::vector<double> pts;
+      if (!object_points(cur, pts)) pts.clear();
+      it = inner_points.emplace(cur, std::move(pts)).first;
+    }
+    const std::vector<double>& pts = it->second;
+    if (pts.empty()) return true;
+    double tlo[3] = {kInf, kInf, kInf}, thi[3] = {-kInf, -kInf, -kInf};
+    for (size_t i = 0; i + 2 < pts.size(); i += 3) {
+      double p[3] = {pts[i], pts[i + 1], pts[i + 2]};
+      for (size_t k = chain.size(); k-- > 0;) {   // innermost wrapper first: object -> world
+        const rt_hittable& w = H(chain[k]);
+        if (w.kind == RT_TRANSLATE) {             // transform.go:100
+          for (int a = 0; a < 3; ++a) p[a] += w.p[a];
+        } else if (w.kind == RT_ROTATE_Y) {       // transform.go:175-178
+          const double s = w.p[0], c = w.p[1], x = p[0], z = p[2];
+          p[0] = c * x + s * z;
+          p[2] = -s * x + c * z;
+        } else if (w.kind == RT_SCALE) {          // transform.go:426-428
+          for (int a = 0; a < 3; ++a) p[a] *= w.p[a];
+        }
+      }
+      for (int a = 0; a < 3; ++a) { tlo[a] = std::min(tlo[a], p[a]); thi[a] = std::max(thi[a], p[a]); }
+    }
+    for (int a = 0; a < 3; ++a) {
+      if (!std::isfinite(tlo[a]) || !std::isfinite(thi[a])) return true;
+      lo[a] = std::max(lo[a], tlo[a]);
+      hi[a] = std::min(hi[a], thi[a]);
+      if (!(lo[a] <= hi[a])) { lo[a] = tlo[a]; hi[a] = thi[a]; }   // (disjoint: keep the geometry's)
+    }
+    return true;
   }
 
   // Collect a wrapper chain starting at g (outermost first); returns inner.
@@ -584,7 +660,7 @@ struct Flattener {
     }
     S.refs.push_back(ref);
     S.ref_rank.push_back(rank);
-    S.ref_box.push_back((ref >> REF_SHIFT) == uint32_t(PK_INSTANCE) ? instance_cull_box(h, int(ref & REF_MASK))
+    S.ref_box.push_back((ref >> REF_SHIFT) == uint32_t(PK_INSTANCE) ? instance_cull_box(g, h, int(ref & REF_MASK))
                                                                      : infinite_ref_box());
     S.ref_top.push_back(g);
     return true;
@@ -711,9 +787,21 @@ struct Flattener {
       }
       TopObj o{};
       o.g = g; o.rank = rank; o.ntests = ntests;
+      // a transformed object: its tight world box (instance_box), padded like
+      // the culling box so that geometry touching it is never lost to the
+      // fp32 slab test's rounding
+      double tlo[3], thi[3];
+      const bool tight = is_wrapper(h.kind) && instance_box(g, tlo, thi);
+      if (tight) {
+        double ext = 0.0;
+        for (int a = 0; a < 3; ++a)
+          ext = std::max(ext, std::max(thi[a] - tlo[a], std::max(std::fabs(tlo[a]), std::fabs(thi[a]))));
+        const double pad = 1e-5 * ext + 1e-6;
+        for (int a = 0; a < 3; ++a) { tlo[a] -= pad; thi[a] += pad; }
+      }
       for (int a = 0; a < 3; ++a) {
-        o.lo[a] = h.bbox[2 * a];
-        o.hi[a] = h.bbox[2 * a + 1];
+        o.lo[a] = tight ? tlo[a] : h.bbox[2 * a];
+        o.hi[a] = tight ? thi[a] : h.bbox[2 * a + 1];
         o.c[a] = 0.5 * (o.lo[a] + o.hi[a]);
         if (!std::isfinite(o.c[a])) { o.lo[a] = -kInf; o.hi[a] = kInf; o.c[a] = 0.0; }
       }

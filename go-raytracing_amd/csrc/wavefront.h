@@ -84,6 +84,9 @@ enum : uint8_t { KC_EXTEND = 0, KC_SHADE = 1, KC_SHADOW = 2, KC_OTHER = 3 };
 // Counter blocks (16 x u64 each): one per kernel class.
 constexpr int CNT_BLOCK = 24;
 
+#ifdef RTG_GUARD
+hipError_t guard_report(unsigned int out[4]);   // diagnostic build: first bad index of the renders
+#endif
 // as[t] / sts[t] for t < plan.num_twins: each twin's buffers and stream.
 hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
                             const WavePlan& plan, int stack, bool count, float* out, int accumulate);

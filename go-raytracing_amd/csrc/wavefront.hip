@@ -269,8 +269,12 @@ __device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, u
 // compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 
+// k_shade at 4 waves per SIMD (128 VGPRs, 2 of them spilled): CornellBoxLucy
+// 1749 -> 1783 Msamples/s against the compiler's own choice (130 VGPRs, 3
+// waves); the shading loop waits on its dependent hit -> triangle / instance
+// reads, so occupancy pays once the spill cost is this small.
 #ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 1
+#define RTG_SHADE_WAVES 4
 #endif
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
 // and this kernel initialises the slot's radiance in Lout.
@@ -353,8 +357,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
       const float time = ray_time(key);
       const uint32_t kh = asu(h.y);
 #ifdef RTG_GUARD
-      if (kh == 0xFFFFFFFFu && atomicAdd(&rtg_guard_hits, 1) < 16)
-        printf("RTG_GUARD site 50: hit %u of %u never written (bounce %u)\n", i, n, bounce);
+      if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
 #endif
       if (kh == 0u) {                                            // miss (camera.go:451-466)
         V3 bg;
@@ -823,6 +826,18 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
   }
   return hipGetLastError();
 }
+
+#ifdef RTG_GUARD
+// count, site, index, length of the first bad index since the last call
+// (then cleared); blocks until the device is idle.
+hipError_t guard_report(unsigned int out[4]) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rtg_guard_rec), 4 * sizeof(unsigned int));
+  const unsigned int zero[4] = {0u, 0u, 0u, 0u};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rtg_guard_rec), zero, sizeof zero);
+  return e;
+}
+#endif
 
 hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
                             const WavePlan& plan, int stack, bool count, float* out, int accumulate) {

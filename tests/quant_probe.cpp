@@ -7,8 +7,14 @@
 //      inside a child box from up to 20 node magnitudes away (grazing edges
 //      and corners included), the traversal's quantised test
 //      (device_common.h: fma(q, inv * step, (origin - o) * inv), fmaxf/fminf)
-//      accepts the child with an interval that holds the aimed point.
-// Prints one JSON line; exit code 0 iff no violation.
+//      accepts the child with an interval that holds the aimed point;
+//   3. outside that envelope (measured, not asserted): rays from 10^2 to
+//      10^5 node magnitudes away.  There the aimed point itself is lost in
+//      the rounding of o, so the reference is the fp32 format's own slab test
+//      on the child's DNode4 box (device_common.h, fp32 branch): far_fail
+//      counts rays that box accepts but the quantised test rejects or
+//      narrows (rtgpu.h documents the envelope).
+// Prints one JSON line; exit code 0 iff no violation of 1 and 2.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -22,7 +28,7 @@ int main(int argc, char** argv) {
   const int nodes = argc > 1 ? atoi(argv[1]) : 20000;
   std::mt19937_64 rng(12345);
   std::uniform_real_distribution<double> U(0.0, 1.0);
-  long contain_fail = 0, slab_fail = 0, rays = 0, unused_fail = 0;
+  long contain_fail = 0, slab_fail = 0, rays = 0, unused_fail = 0, far_rays = 0, far_fail = 0;
   const float inf = HUGE_VALF;
   for (int it = 0; it < nodes; ++it) {
     // node magnitude and child size span many decades (world walls to mesh leaves)
@@ -59,7 +65,8 @@ int main(int argc, char** argv) {
         contain_fail += !(pl <= double(lo4[a][c]) - m && ph >= double(hi4[a][c]) + m);
       }
     // rays at points on / inside the used children
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < 12; ++r) {
+      const bool far = r >= 8;   // outside the documented envelope
       const int c = int(U(rng) * used);
       double P[3];
       for (int a = 0; a < 3; ++a) {
@@ -67,7 +74,8 @@ int main(int argc, char** argv) {
         const double u = U(rng);
         P[a] = u < 0.3 ? l : u < 0.6 ? h : l + (h - l) * U(rng);   // faces, edges, corners
       }
-      const double dist = mag * std::pow(10.0, -2.0 + 3.3 * U(rng));   // up to 20 magnitudes away
+      const double dist = far ? mag * std::pow(10.0, 2.0 + 3.0 * U(rng))    // 10^2..10^5 magnitudes away
+                              : mag * std::pow(10.0, -2.0 + 3.3 * U(rng));  // up to 20 magnitudes away
       double dir[3], len = 0.0;
       for (double& v : dir) { v = U(rng) * 2.0 - 1.0; len += v * v; }
       len = std::sqrt(len);
@@ -94,16 +102,33 @@ int main(int argc, char** argv) {
         ta = std::fmax(ta, std::fma(qf(nr[a]), B[a], A[a]));
         tb = std::fmin(tb, std::fma(qf(fr[a]), B[a], A[a]));
       }
+      const bool ok = tb > ta && ta <= 1.0f + 0x1p-20f && tb >= 1.0f - 0x1p-20f;
+      if (far) {
+        // the fp32 format's test of the same child: planes picked by the
+        // direction's sign, (plane - o) * inv, fmaxf / fminf from [0, inf]
+        float fa = 0.0f, fb = inf;
+        for (int a = 0; a < 3; ++a) {
+          const bool s = std::signbit(inv[a]);
+          const float np = s ? hi4[a][c] : lo4[a][c], fp = s ? lo4[a][c] : hi4[a][c];
+          fa = std::fmax(fa, (np - o[a]) * inv[a]);
+          fb = std::fmin(fb, (fp - o[a]) * inv[a]);
+        }
+        if (fb > fa) {
+          ++far_rays;
+          far_fail += !(tb > ta && ta <= fa && tb >= fb);
+        }
+        continue;
+      }
       ++rays;
       // P itself is only float-close to o + d: allow 2^-20 relative in t
-      if (!(tb > ta && ta <= 1.0f + 0x1p-20f && tb >= 1.0f - 0x1p-20f)) {
+      if (!ok) {
         if (getenv("QP_VERBOSE") && slab_fail < 8)
           fprintf(stderr, "fail mag %g size %g dist %g ta %.9g tb %.9g\n", mag, size, dist, ta, tb);
         ++slab_fail;
       }
     }
   }
-  printf("{\"nodes\": %d, \"rays\": %ld, \"contain_fail\": %ld, \"unused_fail\": %ld, \"slab_fail\": %ld}\n", nodes, rays,
-         contain_fail, unused_fail, slab_fail);
+  printf("{\"nodes\": %d, \"rays\": %ld, \"contain_fail\": %ld, \"unused_fail\": %ld, \"slab_fail\": %ld, "
+         "\"far_rays\": %ld, \"far_fail\": %ld}\n", nodes, rays, contain_fail, unused_fail, slab_fail, far_rays, far_fail);
   return contain_fail || unused_fail || slab_fail ? 1 : 0;
 }

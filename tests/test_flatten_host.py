@@ -105,6 +105,11 @@ def test_node_quantiser_is_conservative(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     info = json.loads(r.stdout)
     assert info["rays"] == 160000 and info["contain_fail"] == info["unused_fail"] == info["slab_fail"] == 0, info
+    # outside the envelope rtgpu.h documents (rays 10^2..10^5 node magnitudes
+    # away): how often the quantised test loses a box the fp32 test keeps
+    assert info["far_rays"] > 0
+    print(f"quant8 vs fp32 boxes, rays 10^2..10^5 node magnitudes away: {info['far_fail']} of "
+          f"{info['far_rays']} accepted boxes lost or narrowed")
 
 
 @pytest.mark.parametrize("name,batch", [("cornell-lucy", 1), ("random", 0), ("cornell-smoke", 0), ("hdri-nee", 0),

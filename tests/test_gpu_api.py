@@ -72,19 +72,25 @@ def test_node_format_option(g):
     """RT_OPT_NODE_FORMAT: only RT_NODES_FP32 / RT_NODES_QUANT8 are accepted;
     a quantised upload renders the same frame as the fp32 one on a scene
     whose hits sit well inside the boxes' margins (CornellBox, 4 spp), and a
-    RotateX/Z scene silently keeps its fp32 nodes."""
+    RotateX/Z scene silently keeps its fp32 nodes: its quant8 upload holds no
+    quantised node array (the same device bytes as its fp32 upload), while
+    CornellBox's holds one more array (64 B per node)."""
     c = g.Context(0)
     try:
         with pytest.raises(g.RTError):
             c.set_option(g.RT_OPT_NODE_FORMAT, 7)
-        frames = {}
+        frames, nbytes, nodes = {}, {}, {}
         for fmt in ("fp32", "quant8"):
             c.set_node_format(fmt)
             for name in ("cornell", "cornell-rotations"):
                 s = g.Scene(name, width=48)
                 c.upload(s.desc)
+                info = c.info()
+                nbytes[fmt, name], nodes[name] = info.device_bytes, info.nodes
                 frames[fmt, name], _ = c.render(s.camera, g.make_params(4, 5, seed=3))
         for name in ("cornell", "cornell-rotations"):
             assert np.array_equal(frames["fp32", name], frames["quant8", name]), name
+        assert nbytes["quant8", "cornell-rotations"] == nbytes["fp32", "cornell-rotations"]
+        assert nbytes["quant8", "cornell"] >= nbytes["fp32", "cornell"] + 64 * nodes["cornell"]
     finally:
         c.close()
