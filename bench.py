@@ -64,6 +64,9 @@ SHADE_END_OUT = 16           # Lout of a sample, zeroed / set at bounce 0 (emiss
 SHADE_JOB_OUT = 52           # NEE job: origin, area dir, info, contribution (+48 with HDRI IS: dir, contribution, throughput)
 SHADOW_JOB_IO = 36           # job origin, area dir in, visibility out (+20 with HDRI IS: dir, info)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+# ranks deal the 32x32 buckets cut into 16x16 tiles round-robin (finer grain
+# than whole buckets: the centre-heavy cost spreads more evenly)
+SHARD_TILE = int(os.environ.get("RTGPU_SHARD_TILE", "16"))
 
 # BASELINE.json configs run on the GPU (C1 SimpleScene is the CPU plumbing case).
 CONFIGS = {
@@ -294,7 +297,7 @@ class Workload:
         self.seed = seed
         self.buckets = g.generate_buckets(self.W, self.H, 32)
         self.params = g.make_params(self.spp, self.depth, seed=seed,
-                                    buckets=g.shard_buckets(self.buckets, D.rank, D.world))
+                                    buckets=g.shard_buckets(self.buckets, D.rank, D.world, SHARD_TILE))
         self.accum = torch.zeros(self.H * self.W * 3, dtype=torch.float32, device=D.dev)
         self.stream = torch.cuda.current_stream(D.dev)
         self.kernel_ms, self.kernel_times = [], []
@@ -500,7 +503,7 @@ def main():
         for n in (2, 4, 8):
             runs = []
             for r in range(n):
-                p = g.make_params(spp, depth, seed=args.seed, buckets=g.shard_buckets(w.buckets, r, n))
+                p = g.make_params(spp, depth, seed=args.seed, buckets=g.shard_buckets(w.buckets, r, n, SHARD_TILE))
                 runs.append(min(timed_render(p) for _ in range(2)))
             shard_ms = [x[0] for x in runs]
             mx, mean = max(shard_ms), float(np.mean(shard_ms))
@@ -508,7 +511,8 @@ def main():
                                 "predicted_speedup": round(full[0] / mx, 3),
                                 "shard_device_ms": [round(x[1], 2) for x in runs],
                                 "shard_trav_shade_ms": [round(x[2], 2) for x in runs]}
-        balance["note"] = ("round-robin 32x32 bucket shards (shard_buckets) timed one after another on this GPU, "
+        balance["note"] = (f"round-robin shards of the 32x32 buckets cut into {SHARD_TILE}x{SHARD_TILE} tiles "
+                           "(shard_buckets) timed one after another on this GPU, "
                            "host clock around render + sync; predicted speed-up = full frame / slowest shard, "
                            "excluding the RCCL reduce of the frame")
 

@@ -183,6 +183,10 @@ def rtgpu() -> C.CDLL:
         lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
         lib.rt_primary_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32), C.POINTER(I32),
                                         C.POINTER(C.c_float)]
+        if hasattr(lib, "rt_render_rgba8"):
+            lib.rt_render_rgba8.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
+                                            C.POINTER(C.c_uint8), C.POINTER(RtStats)]
+            lib.rt_read_frame_sums.argtypes = [P, C.POINTER(C.c_float), C.c_int64]
         if hasattr(lib, "rt_extend_first_hits"):
             lib.rt_extend_first_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32),
                                                  C.POINTER(I32), C.POINTER(C.c_float)]
@@ -337,11 +341,25 @@ def generate_buckets(width: int, height: int, bucket_size: int = 32):
     return bs
 
 
-def shard_buckets(buckets, rank: int, world: int):
+def split_buckets(buckets, tile: int = 16):
+    """Each bucket cut into tile x tile sub-buckets, in bucket order (the
+    kernels' own work tiles are 16x16, api.cpp make_tiles)."""
+    out = []
+    for x, y, w, h in buckets:
+        for ty in range(y, y + h, tile):
+            for tx in range(x, x + w, tile):
+                out.append((tx, ty, min(tile, x + w - tx), min(tile, y + h - ty)))
+    return out
+
+
+def shard_buckets(buckets, rank: int, world: int, tile: int = 0):
     """Round-robin tile sharding across ranks (bucket k -> rank k mod world):
     the centre-heavy cost of the centre-out bucket order is spread evenly
-    (SURVEY.md §8(e)).  The RNG is keyed by global pixel id, so the combined
-    frame is identical for any world size."""
+    (SURVEY.md §8(e)).  tile > 0 deals tile x tile sub-buckets instead (finer
+    grain, better balance).  The RNG is keyed by global pixel id, so the
+    combined frame is identical for any world size and grain."""
+    if tile:
+        buckets = split_buckets(buckets, tile)
     return [b for i, b in enumerate(buckets) if i % world == rank]
 
 
@@ -420,6 +438,21 @@ class Context:
         st = RtStats()
         self._check(self._lib.rt_render(self._h, C.byref(camera), C.byref(params), _f32p(accum), C.byref(st)))
         return accum, st
+
+    def render_rgba8(self, camera: RtCameraDesc, params: RtRenderParams):
+        """One progressive pass (rt_render_rgba8): render + device quantisation;
+        returns the (H, W, 4) RGBA8 framebuffer and the stats."""
+        out = np.zeros((camera.image_height, camera.image_width, 4), np.uint8)
+        st = RtStats()
+        self._check(self._lib.rt_render_rgba8(self._h, C.byref(camera), C.byref(params),
+                                              out.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(st)))
+        return out, st
+
+    def frame_sums(self, camera: RtCameraDesc) -> np.ndarray:
+        """The device frame sums behind render_rgba8's framebuffer."""
+        out = np.zeros((camera.image_height, camera.image_width, 3), np.float32)
+        self._check(self._lib.rt_read_frame_sums(self._h, _f32p(out), out.size))
+        return out
 
     def render_device(self, camera: RtCameraDesc, params: RtRenderParams, dev_ptr: int, stream: int = 0):
         self._check(self._lib.rt_render_device(self._h, C.byref(camera), C.byref(params), C.c_void_p(dev_ptr),

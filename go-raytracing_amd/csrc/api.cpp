@@ -85,6 +85,10 @@ struct rt_ctx {
   // round-robin over all of them (bucket_renderer.go:193-213's worker pool,
   // one GPU per worker)
   std::vector<rt_ctx*> subs;
+  // rt_render_rgba8: the frame's device sums and RGBA8 framebuffer, kept
+  // between calls (pixels outside a call's buckets keep their values)
+  DevBuf frame, frame_rgba, frame_buckets;
+  size_t frame_n = 0;
   hipEvent_t fan_ev = nullptr;    // caller-stream point the devices' renders start after
   hipEvent_t join_ev = nullptr;   // end of this device's share of a render
 };
@@ -544,8 +548,15 @@ int render_multi(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params*
   if (p->buckets && p->num_buckets > 0) bk.assign(p->buckets, p->buckets + p->num_buckets);
   else if (p->buckets == nullptr) bk = default_buckets(cam->image_width, cam->image_height, 32);
   const size_t n = 1 + ctx->subs.size();
+  // dealt at the kernels' 16x16 tile grain (finer than whole buckets: the
+  // centre-heavy cost spreads more evenly over the devices)
+  std::vector<rt_bucket> tiles;
+  for (const rt_bucket& b : bk)
+    for (int y = b.y; y < b.y + b.height; y += 16)
+      for (int x = b.x; x < b.x + b.width; x += 16)
+        tiles.push_back({x, y, std::min(16, b.x + b.width - x), std::min(16, b.y + b.height - y)});
   std::vector<std::vector<rt_bucket>> share(n);
-  for (size_t i = 0; i < bk.size(); ++i) share[i % n].push_back(bk[i]);
+  for (size_t i = 0; i < tiles.size(); ++i) share[i % n].push_back(tiles[i]);
   HIPCHK(hipEventRecord(ctx->fan_ev, st));
   int rc = fan_out(ctx, [&](int k, rt_ctx* c) -> int { return render_share(c, ctx, cam, p, share[size_t(k)], d_out, st); });
   if (rc) return rc;
@@ -644,6 +655,7 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   if (ctx->err_ev) (void)hipEventDestroy(ctx->err_ev);
   free_buf(ctx->wstate); free_buf(ctx->wq); free_buf(ctx->wpix); free_buf(ctx->wacc);
   free_buf(ctx->wspill);
+  free_buf(ctx->frame); free_buf(ctx->frame_rgba); free_buf(ctx->frame_buckets);
   if (ctx->pix_pinned) (void)hipHostFree(ctx->pix_pinned);
   if (ctx->probe_pinned) (void)hipHostFree(ctx->probe_pinned);
   (void)hipEventDestroy(ctx->pix_ev);
@@ -1055,6 +1067,61 @@ int rt_tonemap_rgba8(rt_ctx* ctx, const float* accum_rgb, int32_t width, int32_t
   HIPCHK(launch_tonemap(static_cast<const float*>(ctx->accum.p), int(n), spp, static_cast<uint8_t*>(ctx->rgba.p),
                         ctx->stream));
   HIPCHK(hipMemcpyAsync(rgba_out, ctx->rgba.p, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return RT_OK;
+}
+
+int rt_render_rgba8(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params, uint8_t* rgba_out,
+                    rt_stats* stats) {
+  if (!ctx || !cam || !params || !rgba_out) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
+  if (params->samples_per_pixel <= 0) return set_err(ctx, RT_ERR_INVALID, "bad samples");
+  const int W = cam->image_width, H = cam->image_height;
+  const size_t n = size_t(W) * H;
+  int rc;
+  if (ctx->frame_n != n) {   // a new frame size: sums and framebuffer start at zero
+    if ((rc = ensure(ctx, ctx->frame, n * 3 * sizeof(float)))) return rc;
+    if ((rc = ensure(ctx, ctx->frame_rgba, n * 4))) return rc;
+    HIPCHK(hipMemsetAsync(ctx->frame.p, 0, n * 3 * sizeof(float), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->frame_rgba.p, 0, n * 4, ctx->stream));
+    ctx->frame_n = n;
+  }
+  std::vector<rt_bucket> bk;
+  if (params->buckets && params->num_buckets > 0) bk.assign(params->buckets, params->buckets + params->num_buckets);
+  else if (params->buckets == nullptr) bk = default_buckets(W, H, 32);
+  for (const rt_bucket& b : bk)
+    if (b.width <= 0 || b.height <= 0 || b.x < 0 || b.y < 0 || b.x + b.width > W || b.y + b.height > H)
+      return set_err(ctx, RT_ERR_INVALID, "bucket outside the image");
+  const auto t0 = std::chrono::steady_clock::now();
+  float* fr = static_cast<float*>(ctx->frame.p);
+  if (ctx->subs.empty()) rc = render_impl(ctx, cam, params, fr, ctx->stream, false, nullptr, nullptr);
+  else rc = render_multi(ctx, cam, params, fr, ctx->stream);
+  if (rc) return rc;
+  if (!bk.empty()) {   // quantise the rendered buckets on the device (bucket_renderer.go:276-285)
+    if ((rc = ensure(ctx, ctx->frame_buckets, bk.size() * sizeof(int4)))) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->frame_buckets.p, bk.data(), bk.size() * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_tonemap_buckets(fr, W, static_cast<const int4*>(ctx->frame_buckets.p), int(bk.size()),
+                                  params->samples_per_pixel, static_cast<uint8_t*>(ctx->frame_rgba.p), ctx->stream));
+  }
+  HIPCHK(hipMemcpyAsync(rgba_out, ctx->frame_rgba.p, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if ((rc = rt_sync(ctx))) return rc;
+  if (stats) {
+    stats->kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    uint64_t px = 0;
+    for (const rt_bucket& b : bk) px += uint64_t(b.width) * uint64_t(b.height);
+    stats->samples = px * uint64_t(params->samples_per_pixel);
+  }
+  return RT_OK;
+}
+
+int rt_read_frame_sums(rt_ctx* ctx, float* accum_out, int64_t num_floats) {
+  if (!ctx || !accum_out) return RT_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->frame_n == 0 || num_floats != int64_t(ctx->frame_n * 3))
+    return set_err(ctx, RT_ERR_INVALID, "no rt_render_rgba8 frame of that size");
+  HIPCHK(hipMemcpyAsync(accum_out, ctx->frame.p, ctx->frame_n * 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return RT_OK;
 }

@@ -91,7 +91,8 @@ struct rts_renderer {
   int bucket_size = 32;
   uint32_t seed = 0;
   std::vector<rt_bucket> buckets;
-  std::vector<float> accum;
+  std::vector<float> accum;       // host copy of the last pass's sums (read on demand)
+  bool accum_valid = true;
   std::vector<uint8_t> framebuffer;
   int current_pass = 0;
   bool completed = false;
@@ -224,14 +225,16 @@ int rts_renderer_render_pass(rts_renderer* r, int32_t pass) {
   p.num_buckets = int32_t(r->buckets.size());
   p.accumulate = 0;   // each pass overwrites (renderBucketWithQuality)
   const auto t0 = std::chrono::steady_clock::now();
-  rt_stats st{};
-  int rc = rt_render(r->ctx, &c, &p, r->accum.data(), &st);
+  // one call per pass: render + quantise on the device, only the RGBA8
+  // framebuffer comes back (the sums stay on the device: rts_renderer_accum
+  // reads them on demand)
+  int rc = rt_render_rgba8(r->ctx, &c, &p, r->framebuffer.data(), nullptr);
   if (rc) { r->error = rt_last_error(r->ctx); return rc; }
-  rc = rt_tonemap_rgba8(r->ctx, r->accum.data(), c.image_width, c.image_height, spp, r->framebuffer.data());
-  if (rc) { r->error = rt_last_error(r->ctx); return rc; }
+  r->accum_valid = false;
   if (pass >= 0 && pass < 3) {
-    r->pass_render_ms[pass] = st.kernel_ms;
     r->pass_wall_ms[pass] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    double k = 0.0;
+    if (rt_last_render_kernel_ms(r->ctx, &k) == RT_OK) r->pass_render_ms[pass] = k;
   }
   r->current_pass = pass + 1;
   if (pass >= 2) {
@@ -251,7 +254,13 @@ int rts_renderer_render_all(rts_renderer* r) {
 
 int32_t rts_renderer_is_completed(const rts_renderer* r) { return r && r->completed ? 1 : 0; }
 const uint8_t* rts_renderer_framebuffer(const rts_renderer* r) { return r ? r->framebuffer.data() : nullptr; }
-const float* rts_renderer_accum(const rts_renderer* r) { return r ? r->accum.data() : nullptr; }
+const float* rts_renderer_accum(rts_renderer* r) {
+  if (!r) return nullptr;
+  if (!r->accum_valid &&
+      rt_read_frame_sums(r->ctx, r->accum.data(), int64_t(r->accum.size())) == RT_OK)
+    r->accum_valid = true;
+  return r->accum.data();
+}
 double rts_renderer_duration_ms(const rts_renderer* r) {
   if (!r) return 0;
   auto e = r->completed ? r->end : std::chrono::steady_clock::now();

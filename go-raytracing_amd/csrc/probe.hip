@@ -48,6 +48,28 @@ __device__ __forceinline__ void hit_ids(const DScene& sc, int kind, int idx, int
   else prim = sc.volume_hidx[idx];
 }
 
+// rt_render_rgba8: the same quantisation for the pixels of a bucket list only
+// (one workgroup per bucket): pixels outside them keep the framebuffer's
+// previous value, as renderBucketWithQuality writes only its bucket.
+__global__ __launch_bounds__(256) void tonemap_buckets_kernel(const float* accum, int width, const int4* buckets,
+                                                              int spp, uint8_t* rgba) {
+  const int4 b = buckets[blockIdx.x];   // x, y, w, h
+  const double sc = 1.0 / double(spp);
+  for (int k = threadIdx.x; k < b.z * b.w; k += blockDim.x) {
+    const size_t i = size_t(b.y + k / b.z) * size_t(width) + size_t(b.x + k % b.z);
+    uint8_t o[4];
+    for (int c = 0; c < 3; ++c) {
+      const double v = double(accum[i * 3 + c]) * sc;
+      double g = v > 0.0 ? sqrt(v) : 0.0;
+      if (g < 0.0) g = 0.0;
+      if (g > 0.999) g = 0.999;
+      o[c] = uint8_t(256.0 * g);
+    }
+    o[3] = 255;
+    reinterpret_cast<uchar4*>(rgba)[i] = make_uchar4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // rt_extend_first_hits: k_extend's hit records (wavefront.hip store_hit:
 // t, kind<<28|idx, instance, refpos) of the pixel list -> ids per pixel.
 __global__ __launch_bounds__(256) void hit_ids_kernel(DScene sc, const float4* hit, const uint32_t* pixels,
@@ -109,6 +131,13 @@ hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, i
     if (q) hipLaunchKernelGGL((primary_kernel<64, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
     else hipLaunchKernelGGL((primary_kernel<64, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_tonemap_buckets(const float* accum, int width, const int4* buckets, int nb, int spp, uint8_t* rgba,
+                                  hipStream_t st) {
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tonemap_buckets_kernel, dim3(nb), dim3(256), 0, st, accum, width, buckets, spp, rgba);
   return hipGetLastError();
 }
 

@@ -137,8 +137,12 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 struct Pool {
   uint32_t cur, end;   // unhanded part of the wave's current run
   bool dry;            // the queue is drained
+  bool tail;           // the queue is nearly drained (runs at their minimum): stop prefetching
 };
 
+#ifndef RTG_TAIL_NO_PREFETCH
+#define RTG_TAIL_NO_PREFETCH 1
+#endif
 // Called by the whole wave (converged).  Lanes with `want` get a queue
 // position (or ITEM_NONE).  A new run is claimed only when the wave's run is
 // used up and at least `refill` lanes want an item.
@@ -148,8 +152,13 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   const uint32_t nw = uint32_t(__popcll(m));
   if (P.dry || nw == 0u) return ITEM_NONE;
   if (P.cur >= P.end) {
-    if (nw < uint32_t(refill)) return ITEM_NONE;
+    // (in the tail any idle lane claims: there is no later batch to wait for)
+    if (nw < uint32_t(P.tail ? 1 : refill)) return ITEM_NONE;
     uint32_t run = (n > P.end ? n - P.end : 0u) / (4u * nwaves);
+    // in the queue's last 256 rays per wave a lane stops holding a prefetched
+    // ray behind its current one: a ray left queued behind another lane's
+    // long traversal would end the kernel that much later
+    P.tail = RTG_TAIL_NO_PREFETCH && run < 64u;
     run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
     const int leader = __ffsll(m) - 1;
     uint32_t base = 0;
@@ -195,7 +204,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
                  a.spill_cap};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
-  Pool P{0u, 0u, false};
+  Pool P{0u, 0u, false, false};
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   float4 po = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pd = po;
   uint32_t pb = 0;
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
                                              0.001f, __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
-    const uint32_t idx = pool_take(pn == ITEM_NONE, P, fetch, n, nwaves, a.refill);
+    const uint32_t idx = pool_take(pn == ITEM_NONE && (p == ITEM_NONE || !P.tail), P, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
       pn = GIX(idx, a.slots, 40);
       if (kFirst) {
@@ -541,7 +550,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
                  a.spill_cap};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
-  Pool Q{0u, 0u, false};
+  Pool Q{0u, 0u, false, false};
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   // current job
   uint32_t key = 0, info = 0, vis = 0;
@@ -589,7 +598,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       }
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
-    const uint32_t idx = pool_take(pn == ITEM_NONE, Q, fetch, n, nwaves, a.refill);
+    const uint32_t idx = pool_take(pn == ITEM_NONE && (p == ITEM_NONE || !Q.tail), Q, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
       pn = GIX(idx, a.slots, 46);
       qp = ldnt(&a.sj_p[pn]);

@@ -32,7 +32,6 @@ type GPUBucketRenderer struct {
 	gpu     *rtgpu.Ctx
 	cam     rtgpu.CameraDesc
 	buckets []rtgpu.Bucket // r.buckets (centre-out order of generateBuckets)
-	accum   []float32      // per-pixel radiance sums of the pass in flight
 	rgba    []byte         // tonemapped frame of the pass in flight
 	seed    uint32
 	err     error // first GPU error (under BucketRenderer.mu); the render stops there
@@ -71,9 +70,7 @@ func (g *GPUBucketRenderer) initGPU(camera *Camera, world Hittable) error {
 	for i, b := range g.BucketRenderer.buckets {
 		g.buckets[i] = rtgpu.Bucket{X: int32(b.X), Y: int32(b.Y), Width: int32(b.Width), Height: int32(b.Height)}
 	}
-	n := camera.ImageWidth * camera.ImageHeight
-	g.accum = make([]float32, 3*n)
-	g.rgba = make([]byte, 4*n)
+	g.rgba = make([]byte, 4*camera.ImageWidth*camera.ImageHeight)
 	return nil
 }
 
@@ -148,19 +145,17 @@ func (g *GPUBucketRenderer) passErr() error {
 // gpuPass renders the current pass in one call over every device (each
 // render deals the buckets round-robin over the context's GPUs and
 // overwrites their sums, as renderBucketWithQuality writes every bucket
-// pixel each pass), tonemaps the frame once on the device with
-// bucket_renderer.go:276-285's quantisation and copies it into the
-// framebuffer bucket by bucket under r.mu, as renderBucketWithQuality does.
+// pixel each pass), quantised on the device with bucket_renderer.go:276-285's
+// formula (rt_render_rgba8: only the RGBA8 frame crosses PCIe), and copies it
+// into the framebuffer bucket by bucket under r.mu, as renderBucketWithQuality
+// does.
 func (g *GPUBucketRenderer) gpuPass() {
 	r := g.BucketRenderer
 	spp, depth := passQuality(r.currentPass, r.camera)
-	w, h := r.camera.ImageWidth, r.camera.ImageHeight
+	w := r.camera.ImageWidth
 	seed := g.seed + uint32(r.currentPass)*0x9E3779B9 // one RNG stream per pass
-	_, err := g.gpu.Render(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
-		Buckets: g.buckets}, g.accum)
-	if err == nil {
-		err = g.gpu.Tonemap(g.accum, w, h, spp, g.rgba)
-	}
+	_, err := g.gpu.RenderRGBA(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
+		Buckets: g.buckets}, g.rgba)
 	r.mu.Lock()
 	if err != nil {
 		g.err = err

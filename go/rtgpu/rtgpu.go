@@ -465,6 +465,37 @@ func (c *Ctx) Render(cam *CameraDesc, p RenderParams, accum []float32) (Stats, e
 	return st, c.check(rc)
 }
 
+// RenderRGBA is one progressive pass as renderBucketWithQuality does it
+// (bucket_renderer.go:257-301): the buckets are rendered into the context's
+// device-resident sums and quantised on the device (:276-285); only the
+// RGBA8 framebuffer (width*height*4 bytes) comes back.  Pixels outside the
+// buckets keep their previous value (rt_render_rgba8).
+func (c *Ctx) RenderRGBA(cam *CameraDesc, p RenderParams, rgba []byte) (Stats, error) {
+	var st Stats
+	if len(rgba) < int(cam.ImageWidth)*int(cam.ImageHeight)*4 {
+		return st, &Error{StatusInvalid, "rgba buffer smaller than width*height*4"}
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	prm := (*C.rt_render_params)(C.calloc(1, C.sizeof_rt_render_params))
+	defer C.free(unsafe.Pointer(prm))
+	prm.samples_per_pixel = C.int32_t(p.SamplesPerPixel)
+	prm.max_depth = C.int32_t(p.MaxDepth)
+	prm.sample_offset = C.int32_t(p.SampleOffset)
+	prm.seed = C.uint32_t(p.Seed)
+	if len(p.Buckets) > 0 {
+		pin.Pin(&p.Buckets[0])
+		prm.buckets = (*C.rt_bucket)(unsafe.Pointer(&p.Buckets[0]))
+		prm.num_buckets = C.int32_t(len(p.Buckets))
+	}
+	if p.Accumulate {
+		prm.accumulate = 1
+	}
+	rc := C.rt_render_rgba8(c.p, (*C.rt_camera_desc)(unsafe.Pointer(cam)), prm,
+		(*C.uint8_t)(unsafe.Pointer(&rgba[0])), (*C.rt_stats)(unsafe.Pointer(&st)))
+	return st, c.check(rc)
+}
+
 // Sync waits for every render enqueued on the context and reports a
 // device-side error of any of them.
 func (c *Ctx) Sync() error { return c.check(C.rt_sync(c.p)) }

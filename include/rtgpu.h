@@ -365,6 +365,21 @@ int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out);
 int rt_tonemap_rgba8(rt_ctx* ctx, const float* accum_rgb, int32_t width, int32_t height,
                      int32_t samples_per_pixel, uint8_t* rgba_out);
 
+/* One progressive pass as the drop-in needs it (renderBucketWithQuality,
+ * bucket_renderer.go:257-301): render the buckets into the context's own
+ * device-resident frame sums (overwrite, or add with params->accumulate),
+ * quantise the rendered buckets' pixels on the device (:276-285) into its
+ * RGBA8 framebuffer, and copy that framebuffer (width*height*4 bytes) to
+ * rgba_out.  Pixels outside the buckets keep their previous RGBA8 value.
+ * Only the 4 B/px framebuffer crosses PCIe (rt_render + rt_tonemap_rgba8
+ * move 28 B/px).  A new image size starts from zero.  Blocks.
+ * stats->kernel_ms is the call's wall time.                               */
+int rt_render_rgba8(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+                    uint8_t* rgba_out, rt_stats* stats);
+/* The frame sums behind rt_render_rgba8's framebuffer (width*height*3
+ * floats), e.g. for SaveImage-side checks.                                 */
+int rt_read_frame_sums(rt_ctx* ctx, float* accum_out, int64_t num_floats);
+
 /* Parity probe: first-bounce closest hit of sample `sample` for every pixel.
  * out_top = hittable index of the top-level object (child of the world BVH
  * leaf), out_prim = hittable index of the primitive (== top for

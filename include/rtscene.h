@@ -63,7 +63,7 @@ int rts_renderer_render_pass(rts_renderer* r, int32_t pass);
 int rts_renderer_render_all(rts_renderer* r);
 int32_t rts_renderer_is_completed(const rts_renderer* r);
 const uint8_t* rts_renderer_framebuffer(const rts_renderer* r); /* W*H*4 RGBA */
-const float* rts_renderer_accum(const rts_renderer* r);         /* last pass sum */
+const float* rts_renderer_accum(rts_renderer* r);               /* last pass sum (read back on demand) */
 double rts_renderer_duration_ms(const rts_renderer* r);
 int rts_renderer_save_png(const rts_renderer* r, const char* path);
 const char* rts_renderer_last_error(const rts_renderer* r);

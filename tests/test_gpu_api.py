@@ -94,3 +94,32 @@ def test_node_format_option(g):
         assert nbytes["quant8", "cornell"] >= nbytes["fp32", "cornell"] + 64 * nodes["cornell"]
     finally:
         c.close()
+
+
+def test_render_rgba8_pass(g, O):
+    """rt_render_rgba8 (one progressive pass, bucket_renderer.go:257-301): the
+    device framebuffer is the reference quantisation (:276-285) of the device
+    sums, bit for bit; the sums equal rt_render's; a later call over a bucket
+    subset rewrites only those buckets' RGBA8 pixels; one and two devices agree."""
+    s = g.Scene("cornell", width=64)
+    cam = s.camera
+    for devices in (None, [0, 0]):
+        c = g.Context(0, devices=devices)
+        try:
+            c.upload(s.desc)
+            p = g.make_params(4, 5, seed=31)
+            rgba, st = c.render_rgba8(cam, p)
+            sums = c.frame_sums(cam)
+            ref, _ = c.render(cam, p)
+            assert np.array_equal(sums, ref)
+            assert np.array_equal(rgba, O.tonemap(sums, 4))
+            assert st.samples == cam.image_width * cam.image_height * 4
+            bk = g.generate_buckets(cam.image_width, cam.image_height, 32)[:1]
+            rgba2, _ = c.render_rgba8(cam, g.make_params(1, 3, seed=7, buckets=bk))
+            x, y, w, h = bk[0]
+            mask = np.zeros(rgba.shape[:2], bool)
+            mask[y:y + h, x:x + w] = True
+            assert np.array_equal(rgba2[~mask], rgba[~mask])
+            assert np.array_equal(rgba2[mask], O.tonemap(c.frame_sums(cam), 1)[mask])
+        finally:
+            c.close()
