@@ -52,9 +52,11 @@ struct WaveArgs {
   uint32_t slots;   // capacity of every per-slot array (RTG_GUARD bounds checks)
 };
 
-// Queue counters, each on its own 128-B line (same-line atomics serialise).
-enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT = 96, CNT_FETCH_SH = 128,
-             CNT_WORDS_Q = 160 };
+// Queue counters, each on its own 128-B line (same-line atomics serialise);
+// the claim counters are 8 each, one per queue segment / XCD (wavefront.hip
+// pool_take, shade_claim), 32 words apart.
+enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT = 96, CNT_FETCH_SH = 352,
+             CNT_SHADE_SEG = 608, CNT_WORDS_Q = 864 };
 
 // Traversal kernels: LDS stack ring of kLdsStack entries per lane, the rest
 // of the depth (up to kStackMax) spills to global memory.

@@ -134,18 +134,49 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 // claims a run of queue positions with one atomic and hands them to its
 // lanes without further atomics; runs shrink as the queue drains so the
 // waves finish together.  Every field is wave-uniform.
-struct Pool {
-  uint32_t cur, end;   // unhanded part of the wave's current run
-  bool dry;            // the queue is drained
-  bool tail;           // the queue is nearly drained (runs at their minimum): stop prefetching
-};
-
+// The queue is cut into kSegs contiguous segments, one per XCD: a wave
+// claims from its own XCD's segment first (HW_REG_XCC_ID), and only when that
+// is drained from the next ones.  Stream positions follow the pixel list
+// (tile by tile), so an XCD's waves trace the rays of one screen region and
+// its 4-MB L2 holds the part of the scene those rays touch.  Each segment has
+// its own claim counter (its own 128-B line).  Which wave traces a ray never
+// changes the ray's result.
 #ifndef RTG_TAIL_NO_PREFETCH
 #define RTG_TAIL_NO_PREFETCH 1
 #endif
+#ifndef RTG_XCD_SEGMENTS
+#define RTG_XCD_SEGMENTS 1
+#endif
+constexpr uint32_t kSegs = 8;
+constexpr uint32_t kSegStride = 32;   // words between the segment counters
+struct Pool {
+  uint32_t cur, end;   // unhanded part of the wave's current run
+  uint32_t seg;        // segment claimed from (starts at this wave's XCD)
+  uint32_t tried;      // segments found drained
+  bool dry;            // every segment is drained
+  bool tail;           // the queue is nearly drained (runs at their minimum): stop prefetching
+};
+__device__ __forceinline__ uint32_t xcc_id() {
+#ifdef RTG_HOST_EMU
+  return 0u;
+#else
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & (kSegs - 1u);
+#endif
+}
+__device__ __forceinline__ Pool pool_init() {
+#if RTG_XCD_SEGMENTS
+  return Pool{0u, 0u, xcc_id(), 0u, false, false};
+#else
+  return Pool{0u, 0u, 0u, 0u, false, false};
+#endif
+}
+
 // Called by the whole wave (converged).  Lanes with `want` get a queue
 // position (or ITEM_NONE).  A new run is claimed only when the wave's run is
-// used up and at least `refill` lanes want an item.
+// used up and at least `refill` lanes want an item.  `ctr` = the kSegs
+// segment counters (kSegStride words apart).
 __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr, uint32_t n, uint32_t nwaves,
                                               int refill) {
   const unsigned long long m = __ballot(want);
@@ -154,20 +185,34 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   if (P.cur >= P.end) {
     // (in the tail any idle lane claims: there is no later batch to wait for)
     if (nw < uint32_t(P.tail ? 1 : refill)) return ITEM_NONE;
-    uint32_t run = (n > P.end ? n - P.end : 0u) / (4u * nwaves);
-    // in the queue's last 256 rays per wave a lane stops holding a prefetched
-    // ray behind its current one: a ray left queued behind another lane's
-    // long traversal would end the kernel that much later
-    P.tail = RTG_TAIL_NO_PREFETCH && run < 64u;
-    run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
+    const uint32_t segs = RTG_XCD_SEGMENTS ? kSegs : 1u;
+    const uint32_t wps = RTG_XCD_SEGMENTS ? (nwaves + kSegs - 1u) / kSegs : nwaves;   // waves per segment
     const int leader = __ffsll(m) - 1;
-    uint32_t base = 0;
-    if (__lane_id() == leader) base = atomicAdd(ctr, run);
-    // wave-uniform: scalar registers for the pool state
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
-    if (base >= n) { P.dry = true; return ITEM_NONE; }
-    P.cur = base;
-    P.end = n - base > run ? base + run : n;
+    for (;;) {
+      const uint32_t lo = uint32_t((uint64_t(n) * P.seg) / segs), hi = uint32_t((uint64_t(n) * (P.seg + 1u)) / segs);
+      const uint32_t from = P.end > lo && P.end <= hi ? P.end : lo;   // last known position in this segment
+      uint32_t run = (hi - from) / (4u * wps);
+      // in a segment's last 256 rays per wave a lane stops holding a
+      // prefetched ray behind its current one: a ray left queued behind
+      // another lane's long traversal would end the kernel that much later
+      P.tail = RTG_TAIL_NO_PREFETCH && run < 64u;
+      run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
+      uint32_t base = 0;
+      if (__lane_id() == leader) base = atomicAdd(ctr + P.seg * kSegStride, run);
+      // wave-uniform: scalar registers for the pool state
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + lo;
+      if (base < hi) {
+        P.cur = base;
+        P.end = hi - base > run ? base + run : hi;
+        break;
+      }
+      // this segment is drained: the next one (a wave every segment's
+      // counter has turned away is done)
+      if (++P.tried >= segs) { P.dry = true; return ITEM_NONE; }
+      P.seg = (P.seg + 1u) & (segs - 1u);
+      P.end = 0u;
+      P.tail = true;   // stealing happens in the tail
+    }
   }
   const uint32_t avail = P.end - P.cur;
   const uint32_t rank = lanes_below(m);
@@ -176,8 +221,6 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   return idx;
 }
 
-// Hit record: t, kind<<28 | idx (0 = miss), instance, TLAS ref position (the
-// top-level object: read by the rt_extend_first_hits parity probe only).
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
   stnt(&hit[p], make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
@@ -197,14 +240,21 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
                                                                 uint32_t* fetch, uint32_t sample_base) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack ring + world ray + hit record
   // next stream's count, the shadow job count and the shadow fetch counter
-  if (blockIdx.x == 0 && threadIdx.x == 0) { *zero_a = 0u; *zero_b = 0u; *zero_c = 0u; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *zero_a = 0u;
+    *zero_b = 0u;
+    for (uint32_t k = 0; k < kSegs; ++k) {
+      zero_c[k * kSegStride] = 0u;                        // the shadow pass's segment counters
+      a.counts[CNT_SHADE_SEG + k * kSegStride] = 0u;      // this bounce's k_shade chunk counters
+    }
+  }
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
                  a.spill_cap};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
-  Pool P{0u, 0u, false, false};
+  Pool P = pool_init();
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   float4 po = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pd = po;
   uint32_t pb = 0;
@@ -274,6 +324,23 @@ __device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, u
   p1 = sb[1] + sw[1][w] + lanes_below(m1);
 }
 
+// k_shade claims its work in 256-path chunks, per block, from the segment of
+// the stream its XCD's k_extend waves traced (pool_take), then from the
+// others: the hit -> triangle / instance reads of shading then find the
+// records the same XCD's L2 just served to the traversal.
+#ifndef RTG_SHADE_SEGMENTS
+#define RTG_SHADE_SEGMENTS 1
+#endif
+__device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks, uint32_t& seg, uint32_t& tried) {
+  for (;;) {
+    const uint32_t lo = uint32_t((uint64_t(nchunks) * seg) / kSegs), hi = uint32_t((uint64_t(nchunks) * (seg + 1u)) / kSegs);
+    const uint32_t c = atomicAdd(ctr + seg * kSegStride, 1u);
+    if (lo + c < hi) return lo + c;
+    if (++tried >= kSegs) return 0xFFFFFFFFu;
+    seg = (seg + 1u) & (kSegs - 1u);
+  }
+}
+
 // kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
 // compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
@@ -313,13 +380,26 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
   const uint32_t gs = gridDim.x * blockDim.x;
   // without lights no k_shadow runs (run_batches): reset the next extend's
   // fetch counter here (this extend has finished claiming)
-  if (sc.num_lights == 0 && blockIdx.x == 0 && threadIdx.x == 0) a.counts[CNT_FETCH_EXT] = 0u;
+  if (sc.num_lights == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (uint32_t k = 0; k < kSegs; ++k) a.counts[CNT_FETCH_EXT + k * kSegStride] = 0u;
   Cnt cnt = {};
   // block-uniform trip count (blockDim 256, gs a multiple of 256): every
   // thread reaches the block_reserve2 barriers
   const uint32_t n_up = (n + 255u) & ~255u;
   uint32_t par = 0;
+#if RTG_SHADE_SEGMENTS
+  (void)gs;
+  __shared__ uint32_t s_chunk[2];   // double-buffered like s_w / s_b
+  uint32_t seg = xcc_id(), tried = 0;
+  for (;; par ^= 1u) {
+    if (threadIdx.x == 0) s_chunk[par] = shade_claim(a.counts + CNT_SHADE_SEG, n_up / blockDim.x, seg, tried);
+    __syncthreads();
+    const uint32_t chunk = s_chunk[par];
+    if (chunk == 0xFFFFFFFFu) break;   // block-uniform
+    const uint32_t i = chunk * blockDim.x + threadIdx.x;
+#else
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += gs, par ^= 1u) {
+#endif
     const bool live = i < n;
     bool cont = false, want_shadow = false;
     uint32_t slot = 0, key = 0, flags = 0, bounce = 0, nstate = 0;
@@ -543,14 +623,15 @@ template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kQuant = false>
 __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
-  if (blockIdx.x == 0 && threadIdx.x == 0) *zero_c = 0u;   // next extend's fetch counter
+  if (blockIdx.x == 0 && threadIdx.x == 0)   // next extend's segment counters
+    for (uint32_t k = 0; k < kSegs; ++k) zero_c[k * kSegStride] = 0u;
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
                  a.spill_cap};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
-  Pool Q{0u, 0u, false, false};
+  Pool Q = pool_init();
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   // current job
   uint32_t key = 0, info = 0, vis = 0;
@@ -676,7 +757,12 @@ __global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int ac
 
 __global__ void k_set_counts(uint32_t* c, uint32_t n) {
   if (threadIdx.x == 0) {
-    c[CNT_STREAM0] = n; c[CNT_STREAM1] = 0u; c[CNT_SHADOW] = 0u; c[CNT_FETCH_EXT] = 0u; c[CNT_FETCH_SH] = 0u;
+    c[CNT_STREAM0] = n; c[CNT_STREAM1] = 0u; c[CNT_SHADOW] = 0u;
+    for (uint32_t k = 0; k < kSegs; ++k) {
+      c[CNT_FETCH_EXT + k * kSegStride] = 0u;
+      c[CNT_FETCH_SH + k * kSegStride] = 0u;
+      c[CNT_SHADE_SEG + k * kSegStride] = 0u;
+    }
   }
 }
 
