@@ -182,8 +182,11 @@ def run_pmc_passes(args) -> dict | None:
         e = {"dispatches": max((len(s) for s in disp[fam].values()), default=0)}
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             fetch, write = per("FETCH_SIZE") * 1024 * 2, per("WRITE_SIZE") * 1024
+            # per dispatch, and over the profiled step (one step: with twin
+            # streams a kernel's launch is two dispatches, kernel_report)
             e.update(fetch_bytes_per_launch=int(fetch), write_bytes_per_launch=int(write),
-                     hbm_bytes_per_launch=int(fetch + write))
+                     hbm_bytes_per_launch=int(fetch + write),
+                     hbm_bytes_step=int(v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024))
         h, m = v.get("TCC_HIT_sum", 0.0), v.get("TCC_MISS_sum", 0.0)
         if h + m > 0:
             e["l2_hit"] = round(h / (h + m), 4)
@@ -372,12 +375,15 @@ def kernel_report(w: Workload, work_k: dict, pmc: dict | None):
         # requested_GBs: the algorithm's bytes over the launch
         # time.  Most of them are served by L2 / the Infinity Cache (the scene
         # is cache-resident), so this is no HBM figure and may exceed the peak.
-        e = {"launches": launches, "ms_total": round(ms_tot, 3), "ms_avg": round(ms_avg, 4),
+        e = {"launches": launches, "twins": int(w.kernel_times[0].get("twins", 1)),
+             "ms_total": round(ms_tot, 3), "ms_avg": round(ms_avg, 4),
              "alg_bytes_per_launch": int(per_launch),
              "requested_GBs": round(per_launch / (ms_avg / 1e3) / 1e9, 2) if ms_avg > 0 else None}
         kp = (pmc or {}).get("kernels", {}).get(k)
         if kp and ms_avg > 0 and "hbm_bytes_per_launch" in kp:
-            tb = kp["hbm_bytes_per_launch"]
+            # a launch covers the whole render's work (rt_last_kernel_times
+            # joins the two twins' dispatches of one bounce into one launch)
+            tb = kp["hbm_bytes_step"] / max(launches, 1) if "hbm_bytes_step" in kp else kp["hbm_bytes_per_launch"]
             e["traffic_bytes_per_launch"] = int(tb)
             e["hbm_GBs"] = round(tb / (ms_avg / 1e3) / 1e9, 2)
             e["hbm_frac"] = round(e["hbm_GBs"] / HBM_PEAK_GBS, 4)
@@ -467,6 +473,7 @@ def main():
                     "measure": "L2->fabric bytes (FETCH_SIZE x 2 + WRITE_SIZE, includes Infinity-Cache hits) / "
                                "HIP-event launch time",
                     "kernel": f"k_{dom}", "kernel_ms_avg": kd["ms_avg"], "launches_per_step": kd["launches"],
+                    "twin_streams": kd.get("twins"),
                     "alg_bytes_per_launch": kd["alg_bytes_per_launch"], "requested_GBs": kd["requested_GBs"],
                     "l2_served": kd.get("l2_served"),
                     "l2_hit": kd.get("l2_hit"), "l2_read_latency_cycles": kd.get("l2_read_latency_cycles"),

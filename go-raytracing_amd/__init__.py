@@ -120,7 +120,7 @@ class RtWorkCounts(C.Structure):
 class RtKernelTimes(C.Structure):
     _fields_ = [("extend_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double),
                 ("extend_launches", C.c_int32), ("shade_launches", C.c_int32), ("shadow_launches", C.c_int32),
-                ("pad", C.c_int32)]
+                ("twins", C.c_int32)]
 
 
 class RtSceneInfo(C.Structure):
@@ -519,7 +519,7 @@ class Context:
     def last_kernel_times(self) -> dict:
         t = RtKernelTimes()
         self._check(self._lib.rt_last_kernel_times(self._h, C.byref(t)))
-        return {n: getattr(t, n) for n, _ in RtKernelTimes._fields_ if n != "pad"}
+        return {n: getattr(t, n) for n, _ in RtKernelTimes._fields_}
 
     def tonemap(self, accum: np.ndarray, spp: int) -> np.ndarray:
         h, w = accum.shape[:2]

@@ -68,7 +68,7 @@ struct rt_ctx {
   size_t opt_slots = 0;
   int opt_refill = 0;
   int opt_blocks = 0;
-  int opt_streams = 0;            // RT_OPT_STREAMS: 1 or 2 twins (0 = automatic: 2)
+  int opt_streams = 0;            // RT_OPT_STREAMS: 1 or 2 twins (0 = automatic: 2 up to kTwinSamples)
   // twins of the last render (render_wave): the second's stream, the join
   // events, and where each twin's hit records and pixels are
   hipStream_t stream2 = nullptr;
@@ -249,6 +249,9 @@ int check_render_error(rt_ctx* ctx, bool wait) {
   return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow in a render (its frame is wrong)");
 }
 
+// Largest render (pixels x spp) that gets twin streams by default.
+constexpr uint64_t kTwinSamples = uint64_t(256) << 20;
+
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
 int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const std::vector<int4>& tiles, float* d_out,
@@ -258,10 +261,17 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // tails overlap the other half's next kernel.  RT_OPT_STREAMS = 1 keeps one.
   static const int env_twins = [] {
     const char* e = getenv("RTGPU_STREAMS");
-    return e ? std::min(2, std::max(1, atoi(e))) : 0;
+    return e && atoi(e) > 0 ? std::min(2, atoi(e)) : 0;   // 0: automatic
   }();
-  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : 2;
-  const int nt = (want_twins >= 2 && tiles.size() >= 2) ? 2 : 1;
+  // Automatic: twins for renders of at most kTwinSamples samples (a 1/2 or
+  // smaller shard of CornellBoxLucy, a progressive pass), where the per-launch
+  // tail is a noticeable share of the launch; one stream above that, where it
+  // is not and a launch's interval is its own kernel's alone.
+  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : 0;
+  uint64_t tile_px = 0;
+  for (const int4& tl : tiles) tile_px += uint64_t(tl.z) * uint64_t(tl.w);
+  const bool small = tile_px * uint64_t(std::max(1, p->samples_per_pixel)) <= kTwinSamples;
+  const int nt = ((want_twins >= 2 || (want_twins == 0 && small)) && tiles.size() >= 2) ? 2 : 1;
   std::vector<uint32_t>& px = ctx->pix_host;
   px.clear();
   uint32_t twin_npix[2] = {0, 0};
@@ -852,8 +862,10 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
   d.needs_uv = 0;
-  for (const DTexture& t : h.textures)
+  for (const DTexture& t : h.textures) {
     if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
+    if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.has_fancy = 1;   // the full tex_value / make_record
+  }
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;
   if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }
@@ -866,6 +878,14 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
       free_scene(ctx);
       return rc;
     }
+  }
+  // the winners' shading records, from the final triangle order (host +
+  // device built)
+  if ((rc = upload_vec(ctx, std::vector<DTriShade>(), &d.tri_shade, d.n_tris))) { free_scene(ctx); return rc; }
+  if (hipError_t te = pack_tri_shade(d.tris, d.tri_aux, const_cast<DTriShade*>(d.tri_shade), d.n_tris, ctx->stream)) {
+    rc = hip_fail(ctx, te, "triangle shading records");
+    free_scene(ctx);
+    return rc;
   }
   build_inst_entries(h);   // BLAS roots are final now
   if ((rc = upload_vec(ctx, h.inst_entries, &d.inst_entry))) { free_scene(ctx); return rc; }
@@ -1044,13 +1064,34 @@ int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out) {
   HIPCHK(hipEventSynchronize(ctx->kev1));   // after both twins' streams joined
   double* ms[3] = {&out->extend_ms, &out->shade_ms, &out->shadow_ms};
   int32_t* nl[3] = {&out->extend_launches, &out->shade_launches, &out->shadow_launches};
-  for (int i = 0; i + 1 < ctx->tev_used; i += 2) {   // (begin, end) per launch
-    const int c = ctx->tev_class[i];
+  out->twins = ctx->num_twins;
+  // (begin, end) of every launch relative to the first event, per kernel
+  // class and twin, in launch order
+  std::vector<std::pair<float, float>> iv[3][2];
+  for (int i = 0; i + 1 < ctx->tev_used; i += 2) {
+    const int c = ctx->tev_class[i] & 15, t = (ctx->tev_class[i] & KC_TWIN1) ? 1 : 0;
     if (c > KC_SHADOW) continue;
-    float f = 0.f;
-    HIPCHK(hipEventElapsedTime(&f, ctx->tev[i], ctx->tev[i + 1]));
-    *ms[c] += f;
-    *nl[c] += 1;
+    float b = 0.f, e = 0.f;
+    HIPCHK(hipEventElapsedTime(&b, ctx->tev[0], ctx->tev[i]));
+    HIPCHK(hipEventElapsedTime(&e, ctx->tev[0], ctx->tev[i + 1]));
+    iv[c][t].push_back({b, e});
+  }
+  for (int c = 0; c < 3; ++c) {
+    // twins: the k-th launches of the two twins are one launch over the
+    // whole render's work; its duration is the union of their intervals
+    const size_t n0 = iv[c][0].size(), n1 = iv[c][1].size(), n = std::max(n0, n1);
+    for (size_t k = 0; k < n; ++k) {
+      float b = 0.f, e = 0.f;
+      bool any = false;
+      for (int t = 0; t < 2; ++t) {
+        if (k >= iv[c][t].size()) continue;
+        const auto& x = iv[c][t][k];
+        if (!any) { b = x.first; e = x.second; any = true; }
+        else { b = std::min(b, x.first); e = std::max(e, x.second); }
+      }
+      *ms[c] += double(e - b);
+      *nl[c] += 1;
+    }
   }
   return RT_OK;
 }

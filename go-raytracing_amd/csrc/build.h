@@ -48,4 +48,8 @@ hipError_t build_mesh_blas(const DeviceBuildJob& job, const DRefBox* boxes, Devi
 // out[i] = quantize_node(in[i]) for i < n.  Synchronous on `st`.
 hipError_t quantize_nodes(const DNode4* in, DNodeQ* out, uint32_t n, hipStream_t st);
 
+// The shading records of the final triangle order: out[i] =
+// make_tri_shade(tris[i], aux[i]) for i < n.  Synchronous on `st`.
+hipError_t pack_tri_shade(const DTri* tris, const DTriAux* aux, DTriShade* out, uint32_t n, hipStream_t st);
+
 }  // namespace rtg

@@ -210,6 +210,11 @@ __global__ __launch_bounds__(256) void k_quantize(const DNode4* in, DNodeQ* out,
   if (i < n) out[i] = quantize_node(in[i]);
 }
 
+__global__ __launch_bounds__(256) void k_tri_shade(const DTri* tris, const DTriAux* aux, DTriShade* out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = make_tri_shade(tris[i], aux[i]);
+}
+
 // Device scratch of one build, freed on every exit path.
 struct Scratch {
   std::vector<void*> ptrs;
@@ -334,6 +339,13 @@ hipError_t build_mesh_blas(const DeviceBuildJob& job, const DRefBox* boxes, Devi
 hipError_t quantize_nodes(const DNode4* in, DNodeQ* out, uint32_t n, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_quantize, dim3(blocks(n)), dim3(256), 0, st, in, out, n);
+  BCHK(hipGetLastError());
+  return hipStreamSynchronize(st);
+}
+
+hipError_t pack_tri_shade(const DTri* tris, const DTriAux* aux, DTriShade* out, uint32_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tri_shade, dim3(blocks(n)), dim3(256), 0, st, tris, aux, out, n);
   BCHK(hipGetLastError());
   return hipStreamSynchronize(st);
 }

@@ -162,6 +162,25 @@ struct alignas(16) DTriAux {   // loaded for the winning triangle only
   float nx, ny, nz; int32_t mat;
 };
 
+// Everything shading needs of a winning triangle in one 64-B record (one
+// L2-line half, never split over two lines): the vertex / edges for the hit
+// point, the normal and the material (DTri + DTriAux; built on the device
+// after any BLAS build, build.hip k_tri_shade).  The traversal keeps its
+// packed 36-B DTri array.
+struct alignas(64) DTriShade {
+  float v0[3], nx;
+  float e1[3], ny;
+  float e2[3], nz;
+  int32_t mat, pad0, pad1, pad2;
+};
+static_assert(sizeof(DTriShade) == 64, "DTriShade: 64 B");
+__host__ __device__ inline DTriShade make_tri_shade(const DTri& t, const DTriAux& a) {
+  DTriShade s{};
+  for (int k = 0; k < 3; ++k) { s.v0[k] = t.v0[k]; s.e1[k] = t.e1[k]; s.e2[k] = t.e2[k]; }
+  s.nx = a.nx; s.ny = a.ny; s.nz = a.nz; s.mat = a.mat;
+  return s;
+}
+
 struct alignas(16) DPlane {    // plane.go:5-10
   float px, py, pz; int32_t mat;
   float nx, ny, nz; int32_t rank;
@@ -282,6 +301,7 @@ struct DScene {
   const DQuad* quads;
   const DTri* tris;
   const DTriAux* tri_aux;
+  const DTriShade* tri_shade;  // per triangle: shading record of the winner (k_shade)
   const DCircle* circles;
   const DPerlin* perlins;
   const DImage* images;

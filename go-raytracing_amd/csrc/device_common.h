@@ -1151,6 +1151,15 @@ __device__ __forceinline__ void set_face(V3 d, V3 outward, Rec& rec) {
   rec.N = rec.front ? outward : neg(outward);
 }
 
+// RTG_TRI_SHADE: a winning triangle's vertex, edges, normal and material
+// come from its 64-B DTriShade record (one request) instead of the 36-B
+// DTri (which straddles two lines 27 % of the time) plus the 16-B DTriAux.
+#ifndef RTG_TRI_SHADE
+#define RTG_TRI_SHADE 0
+#endif
+// kUV = false: the scene has no ImageTexture (sc.needs_uv is 0), so the U/V
+// code is compiled out instead of branched over.
+template <bool kUV = true>
 __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float time) {
   Rec rec;
   rec.u = 0.0f;
@@ -1174,7 +1183,7 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
   const DInstance* in = nullptr;
   if (b.inst >= 0) { in = &sc.instances[GIX(b.inst, sc.n_instances, 21)]; to_object(*in, o, d); }
   // UVs (HitRecord.U/V) only when an ImageTexture needs them
-  const bool uv = sc.needs_uv != 0;
+  const bool uv = kUV && sc.needs_uv != 0;
   if (b.kind != PK_TRI) rec.P = add(o, scale(d, b.t));
   if (b.kind == PK_SPHERE) {
     const DSphere& s = sc.spheres[GIX(b.idx, sc.n_spheres, 22)];
@@ -1211,9 +1220,19 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
       rec.v = (dot(lp, bv) / ci.r + 1.0f) * 0.5f;
     }
   } else {  // PK_TRI
+#if RTG_TRI_SHADE
+    // one 64-B record: vertex, edges, normal, material (DTriShade)
+    const DTriShade& ts = sc.tri_shade[GIX(b.idx, sc.n_tris, 24)];
+    set_face(d, mk(ts.nx, ts.ny, ts.nz), rec);
+    rec.mat = ts.mat;
+    const V3 v0 = ld3(ts.v0), e1 = ld3(ts.e1), e2 = ld3(ts.e2);
+#else
     const DTriAux& ax = sc.tri_aux[GIX(b.idx, sc.n_tris, 24)];
     set_face(d, mk(ax.nx, ax.ny, ax.nz), rec);
     rec.mat = ax.mat;
+    const DTri& tr = sc.tris[GIX(b.idx, sc.n_tris, 36)];
+    const V3 v0 = ld3(tr.v0), e1 = ld3(tr.e1), e2 = ld3(tr.e2);
+#endif
     // Moller-Trumbore (u, v) of the winner (triangle.go:57-101).  The hit
     // point is v0 + u*e1 + v*e2: equal to r.At(t) (triangle.go:97) to ~1e-13
     // in the reference's float64, but in fp32 it lies on the triangle's plane
@@ -1221,8 +1240,6 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
     // next ray (tmin 0.001) then re-hits the surface it left: DESIGN.md §5
     // (measured -0.24 % image-mean bias on CornellBoxLucy vs fp64, -0.02 %
     // with this form).
-    const DTri& tr = sc.tris[GIX(b.idx, sc.n_tris, 36)];
-    const V3 v0 = ld3(tr.v0), e1 = ld3(tr.e1), e2 = ld3(tr.e2);
     const V3 h = cross(d, e2);
     const float f = 1.0f / dot(e1, h);
     const V3 sv = sub(o, v0);
@@ -1267,14 +1284,18 @@ __device__ float perlin_turb(const DPerlin& P, V3 pt, int depth) {
   return fabsf(accum);
 }
 
+// kAll = false: the scene holds no Noise / Image texture (DScene.has_fancy
+// is 0), so those branches are compiled out: the 7-octave Perlin turbulence
+// inlined into the shading kernel costs registers even when never taken.
+template <bool kAll = true>
 __device__ __forceinline__ V3 tex_value(const DScene& sc, int ti, float tu, float tv, V3 p) {
   const DTexture& t = sc.textures[ti];
-  if (t.kind == 3) {                                   // NoiseTexture texture.go:81-85
+  if (kAll && t.kind == 3) {                                   // NoiseTexture texture.go:81-85
     const float s = t.scale * p.z + 10.0f * perlin_turb(sc.perlins[t.table], scale(p, t.scale), 7);
     const float g = 0.5f * (1.0f + sinf(s));
     return mk(g, g, g);
   }
-  if (t.kind == 4) {                                   // ImageTexture image_texture.go:26-41
+  if (kAll && t.kind == 4) {                           // ImageTexture image_texture.go:26-41
     const DImage& im = sc.images[t.table];
     if (im.height <= 0) return mk(0.0f, 1.0f, 1.0f);
     const float cu = tu < 0.0f ? 0.0f : (tu > 1.0f ? 1.0f : tu);

@@ -75,7 +75,8 @@ struct WavePlan {
   uint32_t* probe_host;     // pinned words (one per twin) for the long-tail early exit
   // Per-launch timing (rt_set_kernel_timing): events 2k and 2k+1 are
   // recorded before and after one extend / shade / shadow launch on its
-  // stream; ev_class[2k] names the kernel.
+  // stream; ev_class[2k] names the kernel (low 4 bits, KC_*) and the twin
+  // that launched it (bit 4).
   hipEvent_t* events;       // nullptr: timing off
   uint8_t* ev_class;
   int max_events;
@@ -83,6 +84,7 @@ struct WavePlan {
 };
 
 enum : uint8_t { KC_EXTEND = 0, KC_SHADE = 1, KC_SHADOW = 2, KC_OTHER = 3 };
+constexpr uint8_t KC_TWIN1 = 16;   // ev_class flag: launched by twin 1
 // Counter blocks (16 x u64 each): one per kernel class.
 constexpr int CNT_BLOCK = 24;
 

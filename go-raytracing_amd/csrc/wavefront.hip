@@ -342,7 +342,8 @@ __device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks,
 }
 
 // kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
-// compiled in); kFancy: Metal / Dielectric / Isotropic materials present.
+// compiled in); kFancy: Metal / Dielectric / Isotropic materials or Noise /
+// Image textures present (DScene.has_fancy).
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 
 // k_shade at 4 waves per SIMD (128 VGPRs, 2 of them spilled): CornellBoxLucy
@@ -352,10 +353,19 @@ constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 4
 #endif
+// The lean variant (kFancy false: Lambertian / DiffuseLight with solid or
+// checker textures, no U/V code) needs 87-93 VGPRs without spills; 5 waves
+// is also the most its LDS tables (31.5 KB per block) allow.  CornellBoxLucy
+// 1835 (all variants at 4 waves, 128 VGPRs, 2 spilled) -> 1871 (lean at 4)
+// -> 1874 Msamples/s (lean at 5), bit-identical frames.
+#ifndef RTG_SHADE_LEAN_WAVES
+#define RTG_SHADE_LEAN_WAVES 5
+#endif
+#define RTG_SHADE_WAVES_FOR(kFancy) ((kFancy) ? RTG_SHADE_WAVES : RTG_SHADE_LEAN_WAVES)
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
 // and this kernel initialises the slot's radiance in Lout.
 template <bool kCount, bool kEnvIS, bool kFancy, bool kFirst>
-__global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+__global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kFancy)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                const uint32_t* count, PathStream ns, uint32_t* ncount,
                                                uint32_t sample_base) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
@@ -465,19 +475,19 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
         Best b{};
         b.t = h.x; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = int(asu(h.z));
         b.refpos = 0; b.primpos = 0;
-        Rec rec = make_record(sc, b, ro, rd, time);
+        Rec rec = make_record<kFancy>(sc, b, ro, rd, time);
         P = rec.P;
         const DMaterial& m = sc.materials[GIX(rec.mat, sc.num_materials, 42)];
         if (kCount) cnt.mat++;
         V3 att = mk(0.0f, 0.0f, 0.0f);
         bool scat = true, use_mis = false;
         if (m.kind == 4) {                                        // DiffuseLight
-          if (allow) add_L(tex_value(sc, m.tex, rec.u, rec.v, rec.P));
+          if (allow) add_L(tex_value<kFancy>(sc, m.tex, rec.u, rec.v, rec.P));
           scat = false;
         } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
           sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
           if (near_zero(sd)) sd = rec.N;
-          att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
+          att = tex_value<kFancy>(sc, m.tex, rec.u, rec.v, rec.P);
           use_mis = sc.num_lights > 0;
         } else if (!kFancy) {
           scat = false;                                           // unreachable: no such material
@@ -505,7 +515,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
           sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
         } else {                                                  // Isotropic material.go:266-270
           sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
-          att = tex_value(sc, m.tex, rec.u, rec.v, rec.P);
+          att = tex_value<kFancy>(sc, m.tex, rec.u, rec.v, rec.P);
         }
         if (scat) {
           if (use_mis) {                                          // camera.go:502-517 (set-up)
@@ -558,7 +568,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(DScene scg, DCam
                 float cth = dot(rec.N, ldir);
                 if (cth > 0.0f) {
                   const DMaterial& lm = sc.materials[lt.mat];
-                  V3 em = lm.kind == 4 ? tex_value(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
+                  V3 em = lm.kind == 4 ? tex_value<kFancy>(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
                   float area = len(cross(ld3(lt.u), ld3(lt.v)));
                   float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
                   if (!(cl < 0.001f)) {
@@ -865,7 +875,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
 #endif
         // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
-        if ((e = mark_begin(plan, KC_EXTEND, st)) != hipSuccess) return e;
+        if ((e = mark_begin(plan, KC_EXTEND | (t ? KC_TWIN1 : 0), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
@@ -874,7 +884,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_extend", b, st);
-        if ((e = mark_begin(plan, KC_SHADE, st)) != hipSuccess) return e;
+        if ((e = mark_begin(plan, KC_SHADE | (t ? KC_TWIN1 : 0), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh[t]), dim3(256), 0, st, sc, cam, a, a.s[c],
                              cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
@@ -887,7 +897,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         // camera.go:502), so the shadow and apply launches are skipped; k_shade
         // then resets the next extend's fetch counter itself
         if (nee) {
-          if ((e = mark_begin(plan, KC_SHADOW, st)) != hipSuccess) return e;
+          if ((e = mark_begin(plan, KC_SHADOW | (t ? KC_TWIN1 : 0), st)) != hipSuccess) return e;
           hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd[t]), dim3(256), 0, st, sc, a,
                              cnt_shadow, fetch_sh, fetch_ext);
           if ((e = mark_end(plan, st)) != hipSuccess) return e;

@@ -222,10 +222,14 @@ typedef struct rt_work_counts {
 } rt_work_counts;
 
 /* Summed per-launch durations of the wavefront kernels of the last render
- * (HIP events on the render stream; rt_set_kernel_timing(ctx, 1) first).  */
+ * (HIP events on the launch's stream; rt_set_kernel_timing(ctx, 1) first).
+ * With twin streams (twins = 2, RT_OPT_STREAMS) the two twins' launches of
+ * one kernel and bounce run concurrently on disjoint halves of the pixels:
+ * they count as one launch whose duration is the union of the two
+ * intervals, so a launch always covers the whole render's work.          */
 typedef struct rt_kernel_times {
   double extend_ms, shade_ms, shadow_ms;
-  int32_t extend_launches, shade_launches, shadow_launches, pad;
+  int32_t extend_launches, shade_launches, shadow_launches, twins;
 } rt_kernel_times;
 
 /* Sizes of the flattened device scene (rt_scene_get_info). */
@@ -300,9 +304,10 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
  *     of rays (default 16).
  *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups).
- *   RT_OPT_STREAMS: 2 (default) renders the bucket tiles as two halves on
- *     two HIP streams whose kernels overlap each other's tails; 1 keeps one
- *     stream.                                                              */
+ *   RT_OPT_STREAMS: 2 renders the bucket tiles as two halves on two HIP
+ *     streams whose kernels overlap each other's tails; 1 keeps one stream;
+ *     0 (default) = 2 for renders of at most 2^28 samples (pixels x spp),
+ *     where the launch tails are a noticeable share, else 1.                */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };

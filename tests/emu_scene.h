@@ -28,6 +28,7 @@ struct EmuScene {
   std::vector<std::vector<char>> padded;
   HostScene h;
   std::vector<DNodeQ> qnodes;   // quantised nodes (build.hip k_quantize, same function)
+  std::vector<DTriShade> tri_shade;   // shading records (build.hip k_tri_shade, same function)
   DScene d{};
   DCamera cam{};
   int max_depth = 0;
@@ -68,6 +69,10 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
     for (size_t i = 0; i < h.nodes4.size(); ++i) E.qnodes[i] = quantize_node(h.nodes4[i]);
     d.qnodes = pad(E.qnodes);
   }
+  // (its own aligned vector, with 128 B of slack like every scene array)
+  E.tri_shade.assign(h.tris.size() + 2, DTriShade{});
+  for (size_t i = 0; i < h.tris.size(); ++i) E.tri_shade[i] = make_tri_shade(h.tris[i], h.tri_aux[i]);
+  d.tri_shade = E.tri_shade.data();
   d.leaves = pad(h.leaves); d.tris = pad(h.tris); d.quads = pad(h.quads); d.spheres = pad(h.spheres);
   d.quad_wref = ptr(h.quad_wref); d.sphere_wref = ptr(h.sphere_wref);
   d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
@@ -89,12 +94,14 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
   d.n_volumes = uint32_t(h.volumes.size());
   d.n_circles = uint32_t(h.circles.size());
-  d.needs_uv = 0;
-  for (const DTexture& t : h.textures)
-    if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
   d.has_fancy = 0;
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
+  d.needs_uv = 0;
+  for (const DTexture& t : h.textures) {   // as api.cpp rt_scene_upload
+    if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
+    if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.has_fancy = 1;
+  }
 
   const rt_camera_desc* c = rts_scene_get_camera(E.scn);
   DCamera& cam = E.cam;
