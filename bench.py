@@ -150,7 +150,7 @@ def run_pmc_passes(args) -> dict | None:
              str(args.width), "--aspect", repr(args.aspect), "--spp", str(args.spp), "--depth", str(args.depth),
              "--seed", str(args.seed), "--nodes", args.nodes, "--blas", args.blas]
     tmp = tempfile.mkdtemp(prefix="rtg_pmc_", dir="/tmp")
-    env = dict(os.environ, TMPDIR="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp", RTGPU_STREAMS="1")   # single-stream dispatches (attribution_times)
     vals = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(lambda: defaultdict(set))
     ok = []
@@ -344,7 +344,28 @@ class Workload:
         self.ctx.close()
 
 
-def kernel_report(w: Workload, work_k: dict, pmc: dict | None):
+def attribution_times(w: Workload, steps: int = 2) -> list:
+    """Per-kernel launch times for the roofline, from `steps` extra renders of
+    the same workload on ONE stream (RT_OPT_STREAMS=1).  The timed steps run
+    the default twin streams, whose two halves' kernels share the GPU: a
+    kernel's interval there also holds the other twin's kernels, so it says
+    nothing about that kernel alone.  The profiles' rocprof kernel trace
+    (tools/profile_round.sh) runs the same single-stream attribution."""
+    g = w.g
+    w.ctx.set_option(g.RT_OPT_STREAMS, 1)
+    times = []
+    try:
+        for _ in range(steps):
+            w.accum.zero_()
+            w.ctx.render_device(w.cam, w.params, w.accum.data_ptr(), w.stream.cuda_stream)
+            w.ctx.last_render_kernel_ms()   # waits for the render
+            times.append(w.ctx.last_kernel_times())
+    finally:
+        w.ctx.set_option(g.RT_OPT_STREAMS, 0)
+    return times
+
+
+def kernel_report(w: Workload, work_k: dict, pmc: dict | None, ktimes: list):
     """Per-kernel algorithmic bytes (work counts x per-unit bytes, stream bytes
     included) and achieved GB/s over the HIP-event launch times; HBM traffic
     and its fraction of peak from the PMC profile when it is for this code."""
@@ -368,14 +389,14 @@ def kernel_report(w: Workload, work_k: dict, pmc: dict | None):
     }
     out = {}
     for k in ("extend", "shade", "shadow"):
-        launches = int(np.mean([t[f"{k}_launches"] for t in w.kernel_times]))
-        ms_tot = float(np.mean([t[f"{k}_ms"] for t in w.kernel_times]))
+        launches = int(np.mean([t[f"{k}_launches"] for t in ktimes]))
+        ms_tot = float(np.mean([t[f"{k}_ms"] for t in ktimes]))
         ms_avg = ms_tot / max(launches, 1)
         per_launch = alg[k] / max(launches, 1)
         # requested_GBs: the algorithm's bytes over the launch
         # time.  Most of them are served by L2 / the Infinity Cache (the scene
         # is cache-resident), so this is no HBM figure and may exceed the peak.
-        e = {"launches": launches, "twins": int(w.kernel_times[0].get("twins", 1)),
+        e = {"launches": launches, "twins": int(ktimes[0].get("twins", 1)),
              "ms_total": round(ms_tot, 3), "ms_avg": round(ms_avg, 4),
              "alg_bytes_per_launch": int(per_launch),
              "requested_GBs": round(per_launch / (ms_avg / 1e3) / 1e9, 2) if ms_avg > 0 else None}
@@ -457,7 +478,8 @@ def main():
                     pmc_stale = ref_sum is None or frame_sum is None or abs(ref_sum - frame_sum) > 1e-9 * abs(frame_sum)
                 except (OSError, ValueError):
                     pmc = None
-        kernels = kernel_report(w, work_k, pmc)
+        ktimes = attribution_times(w)
+        kernels = kernel_report(w, work_k, pmc, ktimes)
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
         kd = kernels[dom]
         # The bound: bytes the dominant kernel moves between L2 and the fabric
@@ -471,7 +493,8 @@ def main():
         roofline = {"bound": "hbm", "achieved": kd.get("hbm_GBs"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": kd.get("hbm_frac"), "traffic": kd.get("traffic_bytes_per_launch"),
                     "measure": "L2->fabric bytes (FETCH_SIZE x 2 + WRITE_SIZE, includes Infinity-Cache hits) / "
-                               "HIP-event launch time",
+                               "HIP-event launch time, both from single-stream renders of this workload "
+                               "(RT_OPT_STREAMS=1: the timed twin-stream steps overlap two halves' kernels)",
                     "kernel": f"k_{dom}", "kernel_ms_avg": kd["ms_avg"], "launches_per_step": kd["launches"],
                     "twin_streams": kd.get("twins"),
                     "alg_bytes_per_launch": kd["alg_bytes_per_launch"], "requested_GBs": kd["requested_GBs"],

@@ -68,7 +68,7 @@ struct rt_ctx {
   size_t opt_slots = 0;
   int opt_refill = 0;
   int opt_blocks = 0;
-  int opt_streams = 0;            // RT_OPT_STREAMS: 1 or 2 twins (0 = automatic: 2 up to kTwinSamples)
+  int opt_streams = 0;            // RT_OPT_STREAMS: 1 or 2 twins (0 = automatic: 2)
   // twins of the last render (render_wave): the second's stream, the join
   // events, and where each twin's hit records and pixels are
   hipStream_t stream2 = nullptr;
@@ -249,9 +249,6 @@ int check_render_error(rt_ctx* ctx, bool wait) {
   return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow in a render (its frame is wrong)");
 }
 
-// Largest render (pixels x spp) that gets twin streams by default.
-constexpr uint64_t kTwinSamples = uint64_t(256) << 20;
-
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
 int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const std::vector<int4>& tiles, float* d_out,
@@ -263,15 +260,10 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     const char* e = getenv("RTGPU_STREAMS");
     return e && atoi(e) > 0 ? std::min(2, atoi(e)) : 0;   // 0: automatic
   }();
-  // Automatic: twins for renders of at most kTwinSamples samples (a 1/2 or
-  // smaller shard of CornellBoxLucy, a progressive pass), where the per-launch
-  // tail is a noticeable share of the launch; one stream above that, where it
-  // is not and a launch's interval is its own kernel's alone.
-  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : 0;
-  uint64_t tile_px = 0;
-  for (const int4& tl : tiles) tile_px += uint64_t(tl.z) * uint64_t(tl.w);
-  const bool small = tile_px * uint64_t(std::max(1, p->samples_per_pixel)) <= kTwinSamples;
-  const int nt = ((want_twins >= 2 || (want_twins == 0 && small)) && tiles.size() >= 2) ? 2 : 1;
+  // Automatic = twins: CornellBoxLucy full frame 1770 (one stream) -> 1880
+  // Msamples/s, and the 1/8 shards gain more.
+  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : 2;
+  const int nt = (want_twins >= 2 && tiles.size() >= 2) ? 2 : 1;
   std::vector<uint32_t>& px = ctx->pix_host;
   px.clear();
   uint32_t twin_npix[2] = {0, 0};

@@ -223,8 +223,9 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
 
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
-  stnt(&hit[p], make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
-                       asf(uint32_t(b.refpos))));
+  const float4 r = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
+                               asf(uint32_t(b.refpos)));
+  stnt(&hit[p], r);
 }
 
 // ---------------------------------------------------------------- extend

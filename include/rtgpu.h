@@ -304,10 +304,9 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
  *     of rays (default 16).
  *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups).
- *   RT_OPT_STREAMS: 2 renders the bucket tiles as two halves on two HIP
- *     streams whose kernels overlap each other's tails; 1 keeps one stream;
- *     0 (default) = 2 for renders of at most 2^28 samples (pixels x spp),
- *     where the launch tails are a noticeable share, else 1.                */
+ *   RT_OPT_STREAMS: 2 (default) renders the bucket tiles as two halves on
+ *     two HIP streams whose kernels overlap each other's tails; 1 keeps one
+ *     stream.                                                              */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };

@@ -1,7 +1,9 @@
-// Test-only stand-in for <hip/hip_runtime.h>: lets the host emulations
-// (tests/trav_emu.cpp, tests/wave_emu.cpp) compile the device source
-// (device_common.h, wavefront.hip) for the host, one lane per wave and one
-// lane per workgroup, so the CPU suite can run it under AddressSanitizer.
+// Test-only stand-in for <hip/hip_runtime.h>: lets the host emulation
+// (tests/wave_emu.cpp) compile the device source (device_common.h,
+// wavefront.hip) for the host, one lane per wave and one lane per
+// workgroup, so the CPU suite can run it under AddressSanitizer.  With one
+// lane nothing depends on wave-mates, so schedule effects are out of its
+// reach: tests/test_gpu_determinism.py covers those on the GPU.
 // Never used by the product build (go-raytracing_amd/csrc/Makefile uses hipcc).
 #pragma once
 #include <cmath>

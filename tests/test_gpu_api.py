@@ -123,3 +123,30 @@ def test_render_rgba8_pass(g, O):
             assert np.array_equal(rgba2[mask], O.tonemap(c.frame_sums(cam), 1)[mask])
         finally:
             c.close()
+
+
+def test_kernel_times_pair_twin_launches(g, ctx):
+    """rt_last_kernel_times: with twin streams the two halves' launches of a
+    kernel and bounce count as one launch (their union interval), so both
+    schedules report one extend / shade / shadow launch per bounce; the
+    twins field names the schedule, and the frames are bit-identical."""
+    s = g.Scene("cornell", width=64)
+    cam = s.camera
+    ctx.upload(s.desc)
+    p = g.make_params(8, 5, seed=5)
+    frames, times = {}, {}
+    try:
+        ctx.set_kernel_timing(True)
+        for streams in (1, 2):
+            ctx.set_option(g.RT_OPT_STREAMS, streams)
+            frames[streams], _ = ctx.render(cam, p)
+            times[streams] = ctx.last_kernel_times()
+    finally:
+        ctx.set_option(g.RT_OPT_STREAMS, 0)
+        ctx.set_kernel_timing(False)
+    assert np.array_equal(frames[1], frames[2])
+    for streams, t in times.items():
+        assert t["twins"] == streams
+        for k in ("extend", "shade", "shadow"):
+            assert t[f"{k}_launches"] == 5, (streams, k, t)
+            assert t[f"{k}_ms"] > 0.0
