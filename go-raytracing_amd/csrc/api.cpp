@@ -68,15 +68,15 @@ struct rt_ctx {
   size_t opt_slots = 0;
   int opt_refill = 0;
   int opt_blocks = 0;
-  int opt_streams = 0;            // RT_OPT_STREAMS: 1 or 2 twins (0 = automatic: 2)
+  int opt_streams = 0;            // RT_OPT_STREAMS: 1..kMaxTwins twins (0 = automatic: kDefaultTwins)
   // twins of the last render (render_wave): the second's stream, the join
   // events, and where each twin's hit records and pixels are
-  hipStream_t stream2 = nullptr;
-  hipEvent_t twin_ev0 = nullptr, twin_ev1 = nullptr;
+  hipStream_t twin_st[kMaxTwins - 1] = {};   // twins 1.. (twin 0 runs on the caller's stream)
+  hipEvent_t twin_ev0 = nullptr, twin_end[kMaxTwins - 1] = {};
   int num_twins = 1;
-  const float4* twin_hit[2] = {nullptr, nullptr};
-  const uint32_t* twin_pix[2] = {nullptr, nullptr};
-  uint32_t twin_npix[2] = {0, 0};
+  const float4* twin_hit[kMaxTwins] = {};
+  const uint32_t* twin_pix[kMaxTwins] = {};
+  uint32_t twin_npix[kMaxTwins] = {};
   // device BVH build (RT_BLAS_DEVICE) of the last upload
   uint32_t dev_nodes = 0, dev_leaves = 0;   // nodes / leaves added on the device
   double build_ms = 0.0;                    // wall time of the device builds
@@ -249,6 +249,9 @@ int check_render_error(rt_ctx* ctx, bool wait) {
   return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow in a render (its frame is wrong)");
 }
 
+// Twins per render unless RT_OPT_STREAMS / RTGPU_STREAMS say otherwise.
+constexpr int kDefaultTwins = 2;
+
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
 int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const std::vector<int4>& tiles, float* d_out,
@@ -258,15 +261,15 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // tails overlap the other half's next kernel.  RT_OPT_STREAMS = 1 keeps one.
   static const int env_twins = [] {
     const char* e = getenv("RTGPU_STREAMS");
-    return e && atoi(e) > 0 ? std::min(2, atoi(e)) : 0;   // 0: automatic
+    return e && atoi(e) > 0 ? std::min(kMaxTwins, atoi(e)) : 0;   // 0: automatic
   }();
   // Automatic = twins: CornellBoxLucy full frame 1770 (one stream) -> 1880
   // Msamples/s, and the 1/8 shards gain more.
-  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : 2;
-  const int nt = (want_twins >= 2 && tiles.size() >= 2) ? 2 : 1;
+  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : kDefaultTwins;
+  const int nt = int(std::max<size_t>(1, std::min<size_t>(size_t(want_twins), tiles.size())));
   std::vector<uint32_t>& px = ctx->pix_host;
   px.clear();
-  uint32_t twin_npix[2] = {0, 0};
+  uint32_t twin_npix[kMaxTwins] = {};
   for (int t = 0; t < nt; ++t) {
     const size_t before = px.size();
     for (size_t k = size_t(t); k < tiles.size(); k += size_t(nt)) {
@@ -353,8 +356,9 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   if ((rc = ensure(ctx, ctx->wspill, size_t(nt) * spill_words * sizeof(uint32_t)))) return rc;
   // each twin: kSlotF4 arrays of its own S_t slots, its queue counters and
   // job words, its slice of the pixel list and the fp64 sums, its spill area
-  WaveArgs as[2]{};
-  hipStream_t sts[2] = {st, ctx->stream2};
+  WaveArgs as[kMaxTwins]{};
+  hipStream_t sts[kMaxTwins] = {st};
+  for (int t = 1; t < kMaxTwins; ++t) sts[t] = ctx->twin_st[t - 1];
   float4* fbase = static_cast<float4*>(ctx->wstate.p);
   uint32_t* qbase = static_cast<uint32_t*>(ctx->wq.p);
   uint32_t pix_off = 0;
@@ -424,14 +428,14 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   }
   if (ms) HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(hipEventRecord(ctx->kev0, st));
-  if (nt > 1) {   // the second twin's stream starts after the caller's stream reached here
+  if (nt > 1) {   // the other twins' streams start after the caller's stream reached here
     HIPCHK(hipEventRecord(ctx->twin_ev0, st));
-    HIPCHK(hipStreamWaitEvent(ctx->stream2, ctx->twin_ev0, 0));
+    for (int t = 1; t < nt; ++t) HIPCHK(hipStreamWaitEvent(ctx->twin_st[t - 1], ctx->twin_ev0, 0));
   }
   HIPCHK(launch_wavefront(ctx->dscene, dc, as, sts, plan, stack, count, d_out, p->accumulate ? 1 : 0));
-  if (nt > 1) {   // ... and the caller's stream continues once it has finished
-    HIPCHK(hipEventRecord(ctx->twin_ev1, ctx->stream2));
-    HIPCHK(hipStreamWaitEvent(st, ctx->twin_ev1, 0));
+  for (int t = 1; t < nt; ++t) {   // ... and the caller's stream continues once they have finished
+    HIPCHK(hipEventRecord(ctx->twin_end[t - 1], ctx->twin_st[t - 1]));
+    HIPCHK(hipStreamWaitEvent(st, ctx->twin_end[t - 1], 0));
   }
   HIPCHK(hipEventRecord(ctx->kev1, st));
   ctx->kev_recorded = true;
@@ -573,6 +577,15 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+static bool create_twin_streams(rt_ctx* ctx) {
+  if (hipEventCreateWithFlags(&ctx->twin_ev0, hipEventDisableTiming) != hipSuccess) return false;
+  for (int t = 0; t + 1 < kMaxTwins; ++t)
+    if (hipStreamCreateWithFlags(&ctx->twin_st[t], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->twin_end[t], hipEventDisableTiming) != hipSuccess)
+      return false;
+  return true;
+}
+
 int rt_ctx_create(int device, rt_ctx** out) {
   if (!out) return RT_ERR_INVALID;
   *out = nullptr;
@@ -592,9 +605,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
       hipEventCreateWithFlags(&ctx->pix_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&ctx->probe_pinned), 64) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->fan_ev, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->twin_ev0, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->twin_ev1, hipEventDisableTiming) != hipSuccess ||
+      !create_twin_streams(ctx) ||
       hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess ||
       hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
     delete ctx;
@@ -668,8 +679,10 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev1);
   if (ctx->fan_ev) (void)hipEventDestroy(ctx->fan_ev);
   if (ctx->twin_ev0) (void)hipEventDestroy(ctx->twin_ev0);
-  if (ctx->twin_ev1) (void)hipEventDestroy(ctx->twin_ev1);
-  if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
+  for (int t = 0; t + 1 < kMaxTwins; ++t) {
+    if (ctx->twin_end[t]) (void)hipEventDestroy(ctx->twin_end[t]);
+    if (ctx->twin_st[t]) { (void)hipStreamSynchronize(ctx->twin_st[t]); (void)hipStreamDestroy(ctx->twin_st[t]); }
+  }
   if (ctx->join_ev) (void)hipEventDestroy(ctx->join_ev);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -710,7 +723,7 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
     return RT_OK;
   }
   if (key == RT_OPT_STREAMS) {
-    if (value < 0 || value > 2) return set_err(ctx, RT_ERR_INVALID, "streams must be 0 (default), 1 or 2");
+    if (value < 0 || value > kMaxTwins) return set_err(ctx, RT_ERR_INVALID, "streams must be 0 (default) or 1..4");
     ctx->opt_streams = value;
     return RT_OK;
   }
@@ -1059,9 +1072,9 @@ int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out) {
   out->twins = ctx->num_twins;
   // (begin, end) of every launch relative to the first event, per kernel
   // class and twin, in launch order
-  std::vector<std::pair<float, float>> iv[3][2];
+  std::vector<std::pair<float, float>> iv[3][kMaxTwins];
   for (int i = 0; i + 1 < ctx->tev_used; i += 2) {
-    const int c = ctx->tev_class[i] & 15, t = (ctx->tev_class[i] & KC_TWIN1) ? 1 : 0;
+    const int c = ctx->tev_class[i] & 15, t = (ctx->tev_class[i] >> KC_TWIN_SHIFT) & (kMaxTwins - 1);
     if (c > KC_SHADOW) continue;
     float b = 0.f, e = 0.f;
     HIPCHK(hipEventElapsedTime(&b, ctx->tev[0], ctx->tev[i]));
@@ -1069,13 +1082,14 @@ int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out) {
     iv[c][t].push_back({b, e});
   }
   for (int c = 0; c < 3; ++c) {
-    // twins: the k-th launches of the two twins are one launch over the
-    // whole render's work; its duration is the union of their intervals
-    const size_t n0 = iv[c][0].size(), n1 = iv[c][1].size(), n = std::max(n0, n1);
+    // twins: the k-th launches of the twins are one launch over the whole
+    // render's work; its duration is the union of their intervals
+    size_t n = 0;
+    for (int t = 0; t < kMaxTwins; ++t) n = std::max(n, iv[c][t].size());
     for (size_t k = 0; k < n; ++k) {
       float b = 0.f, e = 0.f;
       bool any = false;
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < kMaxTwins; ++t) {
         if (k >= iv[c][t].size()) continue;
         const auto& x = iv[c][t][k];
         if (!any) { b = x.first; e = x.second; any = true; }

@@ -71,12 +71,12 @@ struct WavePlan {
   int32_t num_cus;
   int32_t max_blocks;       // > 0: cap on the persistent traversal grids (RT_OPT_MAX_BLOCKS)
   int32_t debug_sync;       // RTGPU_DEBUG_SYNC=1: synchronise after every launch, name a failing kernel
-  int32_t num_twins;        // 1 or 2 halves of the pixel list on their own streams (run_batches)
+  int32_t num_twins;        // 1..kMaxTwins parts of the pixel list on their own streams (run_batches)
   uint32_t* probe_host;     // pinned words (one per twin) for the long-tail early exit
   // Per-launch timing (rt_set_kernel_timing): events 2k and 2k+1 are
   // recorded before and after one extend / shade / shadow launch on its
   // stream; ev_class[2k] names the kernel (low 4 bits, KC_*) and the twin
-  // that launched it (bit 4).
+  // that launched it (bits 4-5).
   hipEvent_t* events;       // nullptr: timing off
   uint8_t* ev_class;
   int max_events;
@@ -84,7 +84,10 @@ struct WavePlan {
 };
 
 enum : uint8_t { KC_EXTEND = 0, KC_SHADE = 1, KC_SHADOW = 2, KC_OTHER = 3 };
-constexpr uint8_t KC_TWIN1 = 16;   // ev_class flag: launched by twin 1
+constexpr int KC_TWIN_SHIFT = 4;   // ev_class bits 4-5: the twin that launched it
+// Most halves ("twins") a render's pixel list is split into, each on its own
+// stream (RT_OPT_STREAMS).
+constexpr int kMaxTwins = 4;
 // Counter blocks (16 x u64 each): one per kernel class.
 constexpr int CNT_BLOCK = 24;
 

@@ -719,27 +719,54 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
 // contribution if visible), summed in that order (camera.go:549-558).
 // Without HDRI importance sampling a job carries beta * contribution already;
 // a job whose rays were all occluded adds zero and is skipped.
+// RTG_NEE_UNROLL jobs per thread and iteration: their loads (job words,
+// contribution, then the scattered Lout reads) are in flight together.
+#ifndef RTG_NEE_UNROLL
+#define RTG_NEE_UNROLL 1
+#endif
+template <bool kEnvIS>
+__device__ __forceinline__ void nee_apply_one(const WaveArgs& a, uint32_t k, uint32_t flags, uint32_t vis, float4 ea,
+                                              float4 L4) {
+  float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
+  V3 L;
+  if (kEnvIS) {
+    const float4 pb = ldnt(&a.ne_beta[k]);
+    V3 direct = mk(0.0f, 0.0f, 0.0f);
+    if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+    if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
+    L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
+  } else {
+    L = add(mk(L4.x, L4.y, L4.z), mk(ea.x, ea.y, ea.z));
+  }
+  stnt(Lp, make_float4(L.x, L.y, L.z, 0.0f));
+}
 template <bool kEnvIS>
 __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count) {
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
-    const uint32_t flags = ldnt(&a.sj_info[k]) & 0xFFu, vis = ldnt(&a.sj_vis[k]);
-    if ((flags & vis & 3u) == 0u) continue;
-    const float4 ea = ldnt(&a.ne_a[k]);
-    float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
-    const float4 L4 = ldnt(Lp);
-    V3 L;
-    if (kEnvIS) {
-      const float4 pb = ldnt(&a.ne_beta[k]);
-      V3 direct = mk(0.0f, 0.0f, 0.0f);
-      if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
-      if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
-      L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
-    } else {
-      L = add(mk(L4.x, L4.y, L4.z), mk(ea.x, ea.y, ea.z));
+  constexpr int U = RTG_NEE_UNROLL;
+  for (uint32_t k0 = blockIdx.x * blockDim.x + threadIdx.x; k0 < n; k0 += U * gs) {
+    uint32_t fl[U], vi[U];
+    float4 ea[U], L4[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t k = k0 + uint32_t(u) * gs;
+      fl[u] = 0u; vi[u] = 0u;
+      if (k < n) { fl[u] = ldnt(&a.sj_info[k]) & 0xFFu; vi[u] = ldnt(&a.sj_vis[k]); }
     }
-    stnt(Lp, make_float4(L.x, L.y, L.z, 0.0f));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ea[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (fl[u] & vi[u] & 3u) ea[u] = ldnt(&a.ne_a[k0 + uint32_t(u) * gs]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      L4[u] = ea[u];
+      if (fl[u] & vi[u] & 3u) L4[u] = ldnt(a.Lout + GIX(asu(ea[u].w), a.slots, 47));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (fl[u] & vi[u] & 3u) nee_apply_one<kEnvIS>(a, k0 + uint32_t(u) * gs, fl[u], vi[u], ea[u], L4[u]);
   }
 }
 
@@ -845,7 +872,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
   for (uint32_t s0 = 0; s0 < plan.spp; s0 += plan.samples_per_batch) {
     const uint32_t sb = plan.spp - s0 < plan.samples_per_batch ? plan.spp - s0 : plan.samples_per_batch;
     const uint32_t sample_base = plan.sample_offset + s0;
-    int gext0[2], gext[2], gsh[2], gsd[2], gap[2];
+    int gext0[kMaxTwins], gext[kMaxTwins], gsh[kMaxTwins], gsd[kMaxTwins], gap[kMaxTwins];
     for (int t = 0; t < nt; ++t) {
       const WaveArgs& a = as[t];
       const hipStream_t st = sts[t];
@@ -876,7 +903,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
 #endif
         // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
-        if ((e = mark_begin(plan, KC_EXTEND | (t ? KC_TWIN1 : 0), st)) != hipSuccess) return e;
+        if ((e = mark_begin(plan, uint8_t(KC_EXTEND | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
@@ -885,7 +912,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_extend", b, st);
-        if ((e = mark_begin(plan, KC_SHADE | (t ? KC_TWIN1 : 0), st)) != hipSuccess) return e;
+        if ((e = mark_begin(plan, uint8_t(KC_SHADE | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh[t]), dim3(256), 0, st, sc, cam, a, a.s[c],
                              cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
@@ -898,7 +925,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         // camera.go:502), so the shadow and apply launches are skipped; k_shade
         // then resets the next extend's fetch counter itself
         if (nee) {
-          if ((e = mark_begin(plan, KC_SHADOW | (t ? KC_TWIN1 : 0), st)) != hipSuccess) return e;
+          if ((e = mark_begin(plan, uint8_t(KC_SHADOW | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
           hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd[t]), dim3(256), 0, st, sc, a,
                              cnt_shadow, fetch_sh, fetch_ext);
           if ((e = mark_end(plan, st)) != hipSuccess) return e;

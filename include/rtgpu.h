@@ -223,10 +223,10 @@ typedef struct rt_work_counts {
 
 /* Summed per-launch durations of the wavefront kernels of the last render
  * (HIP events on the launch's stream; rt_set_kernel_timing(ctx, 1) first).
- * With twin streams (twins = 2, RT_OPT_STREAMS) the two twins' launches of
- * one kernel and bounce run concurrently on disjoint halves of the pixels:
- * they count as one launch whose duration is the union of the two
- * intervals, so a launch always covers the whole render's work.          */
+ * With twin streams (twins > 1, RT_OPT_STREAMS) the twins' launches of one
+ * kernel and bounce run concurrently on disjoint parts of the pixels: they
+ * count as one launch whose duration is the union of their intervals, so a
+ * launch always covers the whole render's work.                           */
 typedef struct rt_kernel_times {
   double extend_ms, shade_ms, shadow_ms;
   int32_t extend_launches, shade_launches, shadow_launches, twins;
@@ -304,9 +304,9 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
  *     of rays (default 16).
  *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups).
- *   RT_OPT_STREAMS: 2 (default) renders the bucket tiles as two halves on
- *     two HIP streams whose kernels overlap each other's tails; 1 keeps one
- *     stream.                                                              */
+ *   RT_OPT_STREAMS: 1..4 (default 2): the bucket tiles are dealt to that
+ *     many parts ("twins"), each rendered on its own HIP stream, so one
+ *     part's kernel tails overlap the others' kernels; 1 keeps one stream. */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };

@@ -137,14 +137,14 @@ def test_kernel_times_pair_twin_launches(g, ctx):
     frames, times = {}, {}
     try:
         ctx.set_kernel_timing(True)
-        for streams in (1, 2):
+        for streams in (1, 2, 4):
             ctx.set_option(g.RT_OPT_STREAMS, streams)
             frames[streams], _ = ctx.render(cam, p)
             times[streams] = ctx.last_kernel_times()
     finally:
         ctx.set_option(g.RT_OPT_STREAMS, 0)
         ctx.set_kernel_timing(False)
-    assert np.array_equal(frames[1], frames[2])
+    assert np.array_equal(frames[1], frames[2]) and np.array_equal(frames[1], frames[4])
     for streams, t in times.items():
         assert t["twins"] == streams
         for k in ("extend", "shade", "shadow"):

@@ -35,8 +35,9 @@ def _schedules(npix):
     # (batch slots, refill, max persistent blocks, streams): automatic (two
     # twin streams); three batches per frame with waves that claim only when
     # every lane idles on a small grid, one stream; many small batches
-    # claiming as soon as one lane idles, two streams
-    return [(0, 0, 0, 0), (npix * 6, 64, 37, 1), (npix * 2, 1, 600, 2)]
+    # claiming as soon as one lane idles, two streams; the pixels split over
+    # three and four streams
+    return [(0, 0, 0, 0), (npix * 6, 64, 37, 1), (npix * 2, 1, 600, 2), (npix * 4, 4, 0, 3), (0, 0, 0, 4)]
 
 
 def test_c4_full_mesh_schedule_independent(g, O, lucy):
@@ -103,5 +104,5 @@ def test_schedule_option_validation(g, ctx):
     with pytest.raises(g.RTError):
         ctx.set_option(g.RT_OPT_BATCH_SLOTS, -1)
     with pytest.raises(g.RTError):
-        ctx.set_option(g.RT_OPT_STREAMS, 3)
+        ctx.set_option(g.RT_OPT_STREAMS, 5)
     ctx.set_schedule(0, 0, 0, 0)
