@@ -719,54 +719,27 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
 // contribution if visible), summed in that order (camera.go:549-558).
 // Without HDRI importance sampling a job carries beta * contribution already;
 // a job whose rays were all occluded adds zero and is skipped.
-// RTG_NEE_UNROLL jobs per thread and iteration: their loads (job words,
-// contribution, then the scattered Lout reads) are in flight together.
-#ifndef RTG_NEE_UNROLL
-#define RTG_NEE_UNROLL 1
-#endif
-template <bool kEnvIS>
-__device__ __forceinline__ void nee_apply_one(const WaveArgs& a, uint32_t k, uint32_t flags, uint32_t vis, float4 ea,
-                                              float4 L4) {
-  float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
-  V3 L;
-  if (kEnvIS) {
-    const float4 pb = ldnt(&a.ne_beta[k]);
-    V3 direct = mk(0.0f, 0.0f, 0.0f);
-    if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
-    if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
-    L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
-  } else {
-    L = add(mk(L4.x, L4.y, L4.z), mk(ea.x, ea.y, ea.z));
-  }
-  stnt(Lp, make_float4(L.x, L.y, L.z, 0.0f));
-}
 template <bool kEnvIS>
 __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count) {
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
-  constexpr int U = RTG_NEE_UNROLL;
-  for (uint32_t k0 = blockIdx.x * blockDim.x + threadIdx.x; k0 < n; k0 += U * gs) {
-    uint32_t fl[U], vi[U];
-    float4 ea[U], L4[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t k = k0 + uint32_t(u) * gs;
-      fl[u] = 0u; vi[u] = 0u;
-      if (k < n) { fl[u] = ldnt(&a.sj_info[k]) & 0xFFu; vi[u] = ldnt(&a.sj_vis[k]); }
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
+    const uint32_t flags = ldnt(&a.sj_info[k]) & 0xFFu, vis = ldnt(&a.sj_vis[k]);
+    if ((flags & vis & 3u) == 0u) continue;
+    const float4 ea = ldnt(&a.ne_a[k]);
+    float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
+    const float4 L4 = ldnt(Lp);
+    V3 L;
+    if (kEnvIS) {
+      const float4 pb = ldnt(&a.ne_beta[k]);
+      V3 direct = mk(0.0f, 0.0f, 0.0f);
+      if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+      if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
+      L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
+    } else {
+      L = add(mk(L4.x, L4.y, L4.z), mk(ea.x, ea.y, ea.z));
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      ea[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (fl[u] & vi[u] & 3u) ea[u] = ldnt(&a.ne_a[k0 + uint32_t(u) * gs]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      L4[u] = ea[u];
-      if (fl[u] & vi[u] & 3u) L4[u] = ldnt(a.Lout + GIX(asu(ea[u].w), a.slots, 47));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (fl[u] & vi[u] & 3u) nee_apply_one<kEnvIS>(a, k0 + uint32_t(u) * gs, fl[u], vi[u], ea[u], L4[u]);
+    stnt(Lp, make_float4(L.x, L.y, L.z, 0.0f));
   }
 }
 
