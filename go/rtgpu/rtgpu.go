@@ -89,6 +89,10 @@ const (
 	OptBLASBuilder int32 = 1 // RT_OPT_BLAS_BUILDER
 	OptTLASBuilder int32 = 2 // RT_OPT_TLAS_BUILDER
 	OptNodeFormat  int32 = 3 // RT_OPT_NODE_FORMAT
+	OptBatchSlots  int32 = 4 // RT_OPT_BATCH_SLOTS
+	OptRefill      int32 = 5 // RT_OPT_REFILL
+	OptMaxBlocks   int32 = 6 // RT_OPT_MAX_BLOCKS
+	OptStreams     int32 = 7 // RT_OPT_STREAMS
 	BuildReference int32 = 0 // RT_BLAS_REFERENCE
 	BuildSAH       int32 = 1 // RT_BLAS_SAH
 	BuildDevice    int32 = 2 // RT_BLAS_DEVICE
@@ -335,8 +339,11 @@ func (c *Ctx) check(rc C.int) error {
 	return &Error{int(rc), C.GoString(C.rt_last_error(c.p))}
 }
 
-// SetOption sets a context option (OptBLASBuilder / OptTLASBuilder); it
-// takes effect at the next Upload.
+// SetOption sets a context option (OptBLASBuilder / OptTLASBuilder /
+// OptNodeFormat, or a schedule option: OptBatchSlots, OptRefill,
+// OptMaxBlocks, OptStreams, which never change the image).  The scene
+// options take effect at the next Upload, the schedule options at the next
+// render.
 func (c *Ctx) SetOption(key, value int32) error {
 	return c.check(C.rt_ctx_set_option(c.p, C.int32_t(key), C.int32_t(value)))
 }
