@@ -89,6 +89,7 @@ struct rt_ctx {
   // between calls (pixels outside a call's buckets keep their values)
   DevBuf frame, frame_rgba, frame_buckets;
   size_t frame_n = 0;
+  hipEvent_t twin_off_ev = nullptr;   // twin phase offset (WavePlan::offset_ev)
   hipEvent_t fan_ev = nullptr;    // caller-stream point the devices' renders start after
   hipEvent_t join_ev = nullptr;   // end of this device's share of a render
 };
@@ -136,8 +137,16 @@ int upload_vec(rt_ctx* ctx, const std::vector<T>& v, const T** dst, size_t extra
   hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scene)");
   b.bytes = bytes;
-  e = hipMemset(b.p, 0, bytes);
-  if (e == hipSuccess && !v.empty()) e = hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  // On the context's stream, in order with the kernels upload_one launches
+  // there (k_tri_shade, k_quantize, the device BVH build), which read these
+  // arrays.  (A blocking hipMemcpy from pageable memory may return before its
+  // DMA lands, and the context's non-blocking stream is not ordered after
+  // it: with three contexts uploading at once on one GPU, k_tri_shade read
+  // triangles that were not there yet.)  upload_one synchronises the stream
+  // before it returns, so `v` outlives the copy.
+  e = hipMemsetAsync(b.p, 0, bytes, ctx->stream);
+  if (e == hipSuccess && !v.empty())
+    e = hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
   if (e != hipSuccess) { (void)hipFree(b.p); return hip_fail(ctx, e, "hipMemcpy(scene)"); }
   ctx->scene_bufs.push_back(b);
   ctx->scene_bytes += bytes;
@@ -403,6 +412,11 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   plan.num_cus = ctx->num_cus;
   plan.max_blocks = ctx->opt_blocks;
   plan.num_twins = nt;
+  static const int env_offset = [] {
+    const char* e = getenv("RTGPU_TWIN_OFFSET");
+    return e ? atoi(e) : 0;
+  }();
+  plan.offset_ev = env_offset ? ctx->twin_off_ev : nullptr;
   static const int debug_sync = [] {
     const char* e = getenv("RTGPU_DEBUG_SYNC");
     return e && atoi(e) > 0 ? 1 : 0;
@@ -579,6 +593,7 @@ int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 static bool create_twin_streams(rt_ctx* ctx) {
   if (hipEventCreateWithFlags(&ctx->twin_ev0, hipEventDisableTiming) != hipSuccess) return false;
+  if (hipEventCreateWithFlags(&ctx->twin_off_ev, hipEventDisableTiming) != hipSuccess) return false;
   for (int t = 0; t + 1 < kMaxTwins; ++t)
     if (hipStreamCreateWithFlags(&ctx->twin_st[t], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->twin_end[t], hipEventDisableTiming) != hipSuccess)
@@ -679,6 +694,7 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev1);
   if (ctx->fan_ev) (void)hipEventDestroy(ctx->fan_ev);
   if (ctx->twin_ev0) (void)hipEventDestroy(ctx->twin_ev0);
+  if (ctx->twin_off_ev) (void)hipEventDestroy(ctx->twin_off_ev);
   for (int t = 0; t + 1 < kMaxTwins; ++t) {
     if (ctx->twin_end[t]) (void)hipEventDestroy(ctx->twin_end[t]);
     if (ctx->twin_st[t]) { (void)hipStreamSynchronize(ctx->twin_st[t]); (void)hipStreamDestroy(ctx->twin_st[t]); }
@@ -759,7 +775,8 @@ static int device_builds(rt_ctx* ctx) {
     DevBuf boxes;
     int rc = ensure(ctx, boxes, j.boxes.size() * sizeof(DRefBox));
     if (rc) return rc;
-    hipError_t e = hipMemcpy(boxes.p, j.boxes.data(), j.boxes.size() * sizeof(DRefBox), hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpyAsync(boxes.p, j.boxes.data(), j.boxes.size() * sizeof(DRefBox), hipMemcpyHostToDevice,
+                                  ctx->stream);   // ordered before the build's kernels on the same stream
     DeviceBuildJob job{j.blas, j.tri_first, j.n, {j.lo[0], j.lo[1], j.lo[2]}, {j.hi[0], j.hi[1], j.hi[2]}};
     DeviceBuildResult res{};
     if (e == hipSuccess) e = build_mesh_blas(job, static_cast<const DRefBox*>(boxes.p), tgt, res, ctx->stream);
@@ -773,7 +790,8 @@ static int device_builds(rt_ctx* ctx) {
     ctx->dev_leaves += res.leaves_added;
     need = std::max(need, res.need4);
     h.blas[size_t(j.blas)].root_item = res.root_item;
-    HIPCHK(hipMemcpy(const_cast<DBvh*>(d.blas) + j.blas, &h.blas[size_t(j.blas)], sizeof(DBvh), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(const_cast<DBvh*>(d.blas) + j.blas, &h.blas[size_t(j.blas)], sizeof(DBvh), hipMemcpyHostToDevice,
+                          ctx->stream));
   }
   h.stack_needed = h.tlas_need4 + h.max_leaf_inst + 1 + need + 2;
   if (h.stack_needed > kStackMax)
@@ -894,6 +912,13 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   }
   build_inst_entries(h);   // BLAS roots are final now
   if ((rc = upload_vec(ctx, h.inst_entries, &d.inst_entry))) { free_scene(ctx); return rc; }
+  // every copy and upload kernel has landed before the scene is used (by
+  // any stream) and before the host arrays can change
+  if (hipError_t se = hipStreamSynchronize(ctx->stream)) {
+    rc = hip_fail(ctx, se, "scene upload");
+    free_scene(ctx);
+    return rc;
+  }
   ctx->has_scene = true;
   return RT_OK;
 }

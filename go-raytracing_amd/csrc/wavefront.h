@@ -77,6 +77,9 @@ struct WavePlan {
   // recorded before and after one extend / shade / shadow launch on its
   // stream; ev_class[2k] names the kernel (low 4 bits, KC_*) and the twin
   // that launched it (bits 4-5).
+  // twin phase offset (RT_OPT_TWIN_OFFSET): twin 1 starts once twin 0's
+  // first k_extend has finished, so the twins run different kernels at a time
+  hipEvent_t offset_ev;     // nullptr: no offset
   hipEvent_t* events;       // nullptr: timing off
   uint8_t* ev_class;
   int max_events;

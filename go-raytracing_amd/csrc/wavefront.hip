@@ -144,6 +144,9 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 #ifndef RTG_TAIL_NO_PREFETCH
 #define RTG_TAIL_NO_PREFETCH 1
 #endif
+#ifndef RTG_NO_PREFETCH
+#define RTG_NO_PREFETCH 0   // diagnostic: lanes claim only when idle (no prefetched next ray)
+#endif
 #ifndef RTG_XCD_SEGMENTS
 #define RTG_XCD_SEGMENTS 1
 #endif
@@ -195,7 +198,7 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
       // in a segment's last 256 rays per wave a lane stops holding a
       // prefetched ray behind its current one: a ray left queued behind
       // another lane's long traversal would end the kernel that much later
-      P.tail = RTG_TAIL_NO_PREFETCH && run < 64u;
+      P.tail = RTG_NO_PREFETCH || (RTG_TAIL_NO_PREFETCH && run < 64u);
       run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
       uint32_t base = 0;
       if (__lane_id() == leader) base = atomicAdd(ctr + P.seg * kSegStride, run);
@@ -346,6 +349,18 @@ __device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks,
 // compiled in); kFancy: Metal / Dielectric / Isotropic materials or Noise /
 // Image textures present (DScene.has_fancy).
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
+// The tables k_shade copies to LDS live in dynamic shared memory sized to the
+// scene (shade_lds_bytes; 0 = too large, read from global): a static
+// worst-case allocation (31.5 KB per block) capped the kernel at 5 blocks per
+// CU whatever its registers allowed.
+__host__ __device__ inline bool shade_tables_fit(const DScene& sc) {
+  return sc.num_materials <= kLdsMaterials && sc.num_textures <= kLdsTextures && sc.num_lights <= kLdsLights;
+}
+__host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
+  return shade_tables_fit(sc) ? size_t(sc.num_materials) * sizeof(DMaterial) + size_t(sc.num_textures) * sizeof(DTexture) +
+                                    size_t(sc.num_lights) * sizeof(DLight)
+                              : 0;
+}
 
 // k_shade at 4 waves per SIMD (128 VGPRs, 2 of them spilled): CornellBoxLucy
 // 1749 -> 1783 Msamples/s against the compiler's own choice (130 VGPRs, 3
@@ -358,9 +373,13 @@ constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 // checker textures, no U/V code) needs 87-93 VGPRs without spills; 5 waves
 // is also the most its LDS tables (31.5 KB per block) allow.  CornellBoxLucy
 // 1835 (all variants at 4 waves, 128 VGPRs, 2 spilled) -> 1871 (lean at 4)
-// -> 1874 Msamples/s (lean at 5), bit-identical frames.
+// -> 1874 Msamples/s (lean at 5), bit-identical frames.  With its LDS tables
+// sized to the scene (shade_lds_bytes) the lean variant runs at 7 waves (72
+// VGPRs, 4 spilled): 1896 (5) / 1934 (6) / 1978 (7) / 1928 (8 waves): a
+// 72-VGPR block also fits beside the traversal kernels' 72-VGPR waves when
+// the twin streams overlap them.
 #ifndef RTG_SHADE_LEAN_WAVES
-#define RTG_SHADE_LEAN_WAVES 5
+#define RTG_SHADE_LEAN_WAVES 7
 #endif
 #define RTG_SHADE_WAVES_FOR(kFancy) ((kFancy) ? RTG_SHADE_WAVES : RTG_SHADE_LEAN_WAVES)
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
@@ -372,13 +391,18 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kFancy)) void k_shade(DSce
   // Small scene tables (materials, textures, lights) are read from LDS: they
   // sit on every path's dependent-load chain (hit -> material -> texture,
   // light -> light material -> texture).
-  __shared__ DMaterial s_mat[kLdsMaterials];
-  __shared__ DTexture s_tex[kLdsTextures];
-  __shared__ DLight s_light[kLdsLights];
+#ifdef RTG_HOST_EMU
+  static char s_dyn[kLdsMaterials * sizeof(DMaterial) + kLdsTextures * sizeof(DTexture) + kLdsLights * sizeof(DLight)];
+#else
+  extern __shared__ char s_dyn[];   // shade_lds_bytes(sc) per block (all records 16-B aligned, multiples of 16 B)
+#endif
   __shared__ uint32_t s_w[2][2][4];
   __shared__ uint32_t s_b[2][2];
   DScene sc = scg;
-  if (sc.num_materials <= kLdsMaterials && sc.num_textures <= kLdsTextures && sc.num_lights <= kLdsLights) {
+  if (shade_tables_fit(sc)) {
+    DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
+    DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
+    DLight* const s_light = reinterpret_cast<DLight*>(s_tex + sc.num_textures);
     for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = scg.materials[i];
     for (int i = threadIdx.x; i < sc.num_textures; i += blockDim.x) s_tex[i] = scg.textures[i];
     for (int i = threadIdx.x; i < sc.num_lights; i += blockDim.x) s_light[i] = scg.lights[i];
@@ -841,6 +865,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
   const int cus = plan.num_cus;
   const int nt = plan.num_twins;
   const bool nee = sc.num_lights > 0;
+  const size_t shade_lds = shade_lds_bytes(sc);
   hipError_t e;
   for (uint32_t s0 = 0; s0 < plan.spp; s0 += plan.samples_per_batch) {
     const uint32_t sb = plan.spp - s0 < plan.samples_per_batch ? plan.spp - s0 : plan.samples_per_batch;
@@ -856,7 +881,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
       int max_trav_blocks = int(a.spill_lanes / 256u);
       if (plan.max_blocks > 0 && plan.max_blocks < max_trav_blocks) max_trav_blocks = plan.max_blocks;
       auto cap = [&](int g) { return g < max_trav_blocks ? g : max_trav_blocks; };
-      gsh[t] = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, 0, nslots, cus);
+      gsh[t] = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, shade_lds, nslots, cus);
       gsd[t] = cap(grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus));
       gap[t] = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
       gext0[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, true, kQuant>, 256, 0, nslots, cus));
@@ -876,6 +901,8 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
 #endif
         // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
+        const bool offset = plan.offset_ev && s0 == 0 && b == 0 && nt > 1;
+        if (offset && t == 1 && (e = hipStreamWaitEvent(st, plan.offset_ev, 0)) != hipSuccess) return e;
         if ((e = mark_begin(plan, uint8_t(KC_EXTEND | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
@@ -884,13 +911,14 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
           hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant>), dim3(gext[t]), dim3(256), 0, st, sc, cam, a,
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
+        if (offset && t == 0 && (e = hipEventRecord(plan.offset_ev, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_extend", b, st);
         if ((e = mark_begin(plan, uint8_t(KC_SHADE | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
-          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh[t]), dim3(256), 0, st, sc, cam, a, a.s[c],
+          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
                              cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
         else
-          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh[t]), dim3(256), 0, st, sc, cam, a, a.s[c],
+          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
                              cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_shade", b, st);
