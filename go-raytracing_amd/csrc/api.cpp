@@ -258,8 +258,13 @@ int check_render_error(rt_ctx* ctx, bool wait) {
   return set_err(ctx, RT_ERR_DEVICE, "device traversal stack overflow in a render (its frame is wrong)");
 }
 
-// Twins per render unless RT_OPT_STREAMS / RTGPU_STREAMS say otherwise.
+// Twins per render unless RT_OPT_STREAMS / RTGPU_STREAMS say otherwise: three
+// for renders of more than kThreeTwinSamples samples (pixels x spp), two
+// below.  CornellBoxLucy full frame (405 M samples): one stream 1770, two
+// 1937-1952, three 1967-1970 Msamples/s; its 1/8 shards (51 M) are faster on
+// two (8-way shard prediction 7.00 vs 6.83 on three).
 constexpr int kDefaultTwins = 2;
+constexpr uint64_t kThreeTwinSamples = uint64_t(1) << 28;
 
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
@@ -274,7 +279,10 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   }();
   // Automatic = twins: CornellBoxLucy full frame 1770 (one stream) -> 1880
   // Msamples/s, and the 1/8 shards gain more.
-  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : kDefaultTwins;
+  uint64_t tile_px = 0;
+  for (const int4& tl : tiles) tile_px += uint64_t(tl.z) * uint64_t(tl.w);
+  const int auto_twins = tile_px * uint64_t(std::max(1, p->samples_per_pixel)) > kThreeTwinSamples ? 3 : kDefaultTwins;
+  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : auto_twins;
   const int nt = int(std::max<size_t>(1, std::min<size_t>(size_t(want_twins), tiles.size())));
   std::vector<uint32_t>& px = ctx->pix_host;
   px.clear();
@@ -410,7 +418,12 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   plan.sample_offset = uint32_t(p->sample_offset);
   plan.max_depth = p->max_depth;
   plan.num_cus = ctx->num_cus;
-  plan.max_blocks = ctx->opt_blocks;
+  // RTGPU_MAX_BLOCKS (tuning knob, like RTGPU_SLOTS): the option's default
+  static const int env_blocks = [] {
+    const char* e = getenv("RTGPU_MAX_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : 0;
+  }();
+  plan.max_blocks = ctx->opt_blocks ? ctx->opt_blocks : env_blocks;
   plan.num_twins = nt;
   static const int env_offset = [] {
     const char* e = getenv("RTGPU_TWIN_OFFSET");

@@ -304,9 +304,10 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
  *     of rays (default 16).
  *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups).
- *   RT_OPT_STREAMS: 1..4 (default 2): the bucket tiles are dealt to that
- *     many parts ("twins"), each rendered on its own HIP stream, so one
- *     part's kernel tails overlap the others' kernels; 1 keeps one stream. */
+ *   RT_OPT_STREAMS: 1..4: the bucket tiles are dealt to that many parts
+ *     ("twins"), each rendered on its own HIP stream, so one part's kernel
+ *     tails overlap the others' kernels; 1 keeps one stream.  Default: 3
+ *     for renders of more than 2^28 samples (pixels x spp), else 2.        */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
