@@ -1406,10 +1406,13 @@ __device__ __forceinline__ V3 disk_point(uint32_t key) {   // RandomInUnitDisk (
   return p;
 }
 
-#ifdef RTG_INLINE_SLOW_CAMERA
-__device__ __forceinline__
-#else
+// Inlined: as a call it made the bounce-0 kernels save their live registers
+// around the call site (k_extend<kFirst> 22 VGPRs spilled, 320 B of scratch
+// per lane; inlined 8 and 36 B): CornellBoxLucy 1970 -> 2008 Msamples/s.
+#ifdef RTG_NOINLINE_SLOW_CAMERA
 __device__ __noinline__
+#else
+__device__ __forceinline__
 #endif
 void get_ray_slow(const DCamera& cam, int px, int py, uint32_t key, float offx, float offy,
                                           float time, V3& ro, V3& rd) {
