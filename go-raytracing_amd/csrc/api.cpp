@@ -894,13 +894,13 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
   d.n_volumes = uint32_t(h.volumes.size());
   d.n_circles = uint32_t(h.circles.size());
-  d.has_fancy = 0;
+  d.shade_kind = SHADE_LEAN;   // the k_shade variant (wavefront.hip)
   for (const DMaterial& m : h.materials)
-    if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
+    if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.shade_kind = SHADE_MAT;
   d.needs_uv = 0;
   for (const DTexture& t : h.textures) {
     if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
-    if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.has_fancy = 1;   // the full tex_value / make_record
+    if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.shade_kind = SHADE_FULL;   // the full tex_value / make_record
   }
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;

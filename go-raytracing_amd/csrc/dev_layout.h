@@ -289,6 +289,9 @@ struct alignas(16) DRefBox {
   float hi[3], pad1;
 };
 
+// k_shade variants: the material / texture code a scene needs compiled in.
+enum : int32_t { SHADE_LEAN = 0, SHADE_MAT = 1, SHADE_FULL = 2 };
+
 // Everything the kernels need, passed by value as a kernel argument.
 struct DScene {
   const DNode4* nodes;         // BVH4 nodes, full fp32 boxes (build form; ITEM_NODE indexes it)
@@ -337,7 +340,7 @@ struct DScene {
   int32_t num_textures;
   int32_t stack_needed;
   int32_t has_volumes;
-  int32_t has_fancy;      // a Metal / Dielectric / Isotropic material exists
+  int32_t shade_kind;     // SHADE_LEAN / SHADE_MAT / SHADE_FULL: the k_shade variant (shade_kind_of)
   int32_t needs_uv;       // an ImageTexture exists: hit records carry U/V
   int32_t quant_nodes;    // traverse the quantised DNodeQ nodes (RT_NODES_QUANT8), else DNode4
   // array lengths (bounds checks of the RTG_GUARD diagnostic build)

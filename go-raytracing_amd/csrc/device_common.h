@@ -1286,7 +1286,7 @@ __device__ float perlin_turb(const DPerlin& P, V3 pt, int depth) {
   return fabsf(accum);
 }
 
-// kAll = false: the scene holds no Noise / Image texture (DScene.has_fancy
+// kAll = false: the scene holds no Noise / Image texture (DScene.shade_kind
 // is 0), so those branches are compiled out: the 7-octave Perlin turbulence
 // inlined into the shading kernel costs registers even when never taken.
 template <bool kAll = true>

@@ -346,8 +346,9 @@ __device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks,
 }
 
 // kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
-// compiled in); kFancy: Metal / Dielectric / Isotropic materials or Noise /
-// Image textures present (DScene.has_fancy).
+// compiled in); kShade (DScene.shade_kind): SHADE_LEAN = Lambertian /
+// DiffuseLight with solid or checker textures, SHADE_MAT = also Metal /
+// Dielectric / Isotropic, SHADE_FULL = also Noise / Image textures (and U/V).
 constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 // The tables k_shade copies to LDS live in dynamic shared memory sized to the
 // scene (shade_lds_bytes; 0 = too large, read from global): a static
@@ -381,11 +382,20 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
 #ifndef RTG_SHADE_LEAN_WAVES
 #define RTG_SHADE_LEAN_WAVES 7
 #endif
-#define RTG_SHADE_WAVES_FOR(kFancy) ((kFancy) ? RTG_SHADE_WAVES : RTG_SHADE_LEAN_WAVES)
+// The middle variant (Metal / Dielectric / Isotropic, solid or checker
+// textures: C2, C3, C5) at 7 waves (72 VGPRs, spilling): measured (4 / 5 /
+// 6 / 7 waves) C2 3473 / 3502 / 3473 / 3632, C3 1014 / 1019 / 1022 / 1005,
+// C5 8548 / 8684 / 8751 / 8973 Msamples/s (the full variant at 4 waves:
+// C2 3376, C3 1013, C5 8216).
+#ifndef RTG_SHADE_MAT_WAVES
+#define RTG_SHADE_MAT_WAVES 7
+#endif
+#define RTG_SHADE_WAVES_FOR(kShade) \
+  ((kShade) == SHADE_FULL ? RTG_SHADE_WAVES : (kShade) == SHADE_MAT ? RTG_SHADE_MAT_WAVES : RTG_SHADE_LEAN_WAVES)
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
 // and this kernel initialises the slot's radiance in Lout.
-template <bool kCount, bool kEnvIS, bool kFancy, bool kFirst>
-__global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kFancy)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+template <bool kCount, bool kEnvIS, int kShade, bool kFirst>
+__global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                const uint32_t* count, PathStream ns, uint32_t* ncount,
                                                uint32_t sample_base) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
@@ -500,22 +510,25 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kFancy)) void k_shade(DSce
         Best b{};
         b.t = h.x; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = int(asu(h.z));
         b.refpos = 0; b.primpos = 0;
-        Rec rec = make_record<kFancy>(sc, b, ro, rd, time);
+        Rec rec = make_record<kShade == SHADE_FULL>(sc, b, ro, rd, time);
         P = rec.P;
         const DMaterial& m = sc.materials[GIX(rec.mat, sc.num_materials, 42)];
         if (kCount) cnt.mat++;
         V3 att = mk(0.0f, 0.0f, 0.0f);
         bool scat = true, use_mis = false;
         if (m.kind == 4) {                                        // DiffuseLight
-          if (allow) add_L(tex_value<kFancy>(sc, m.tex, rec.u, rec.v, rec.P));
+          if (allow) add_L(tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P));
           scat = false;
         } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
           sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
           if (near_zero(sd)) sd = rec.N;
-          att = tex_value<kFancy>(sc, m.tex, rec.u, rec.v, rec.P);
+          att = tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P);
           use_mis = sc.num_lights > 0;
-        } else if (!kFancy) {
+        } else if (kShade == SHADE_LEAN) {
           scat = false;                                           // unreachable: no such material
+        } else if (m.kind == 5) {                                 // Isotropic material.go:266-270
+          sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
+          att = tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P);
         } else if (m.kind == 2) {                                 // Metal material.go:113-119
           V3 refl = reflect(rd, rec.N);
           refl = add(unit(refl), scale(random_unit_vector(key, bounce, DOM_SCATTER, 0), m.fuzz));
@@ -538,9 +551,8 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kFancy)) void k_shade(DSce
             refl = rf > rnd(key, ctr(bounce, DOM_FRESNEL, 0));
           }
           sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
-        } else {                                                  // Isotropic material.go:266-270
-          sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
-          att = tex_value<kFancy>(sc, m.tex, rec.u, rec.v, rec.P);
+        } else {
+          scat = false;                                           // unreachable: no such material
         }
         if (scat) {
           if (use_mis) {                                          // camera.go:502-517 (set-up)
@@ -593,7 +605,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kFancy)) void k_shade(DSce
                 float cth = dot(rec.N, ldir);
                 if (cth > 0.0f) {
                   const DMaterial& lm = sc.materials[lt.mat];
-                  V3 em = lm.kind == 4 ? tex_value<kFancy>(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
+                  V3 em = lm.kind == 4 ? tex_value<kShade == SHADE_FULL>(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
                   float area = len(cross(ld3(lt.u), ld3(lt.v)));
                   float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
                   if (!(cl < 0.001f)) {
@@ -859,7 +871,7 @@ static hipError_t mark_end(const WavePlan& plan, hipStream_t st) {
 // compute units those waves free, so the tails overlap with work.  Each
 // pixel belongs to one twin and keeps its sample order: the frame is
 // bit-identical to a one-stream render.
-template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
+template <int STACK, bool kCount, bool kVol, bool kEnvIS, int kShade, bool kQuant>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
                               const WavePlan& plan) {
   const int cus = plan.num_cus;
@@ -881,7 +893,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
       int max_trav_blocks = int(a.spill_lanes / 256u);
       if (plan.max_blocks > 0 && plan.max_blocks < max_trav_blocks) max_trav_blocks = plan.max_blocks;
       auto cap = [&](int g) { return g < max_trav_blocks ? g : max_trav_blocks; };
-      gsh[t] = grid_for((const void*)k_shade<kCount, kEnvIS, kFancy, false>, 256, shade_lds, nslots, cus);
+      gsh[t] = grid_for((const void*)k_shade<kCount, kEnvIS, kShade, false>, 256, shade_lds, nslots, cus);
       gsd[t] = cap(grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus));
       gap[t] = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
       gext0[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, true, kQuant>, 256, 0, nslots, cus));
@@ -915,10 +927,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         RTG_LAUNCHED("k_extend", b, st);
         if ((e = mark_begin(plan, uint8_t(KC_SHADE | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
-          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, true>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
+          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, true>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
                              cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
         else
-          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kFancy, false>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
+          hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, false>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
                              cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_shade", b, st);
@@ -982,15 +994,16 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
   if (plan.max_depth > 0) {
     // the kVol variants also carry the rare primitives (circles)
     const bool vol = sc.has_volumes != 0 || sc.n_circles > 0;
-#define RUN2(S, C, V, Q)                                                           \
-  do {                                                                             \
-    if (envis) {                                                                   \
-      if (fancy) e = run_batches<S, C, V, true, true, Q>(sc, cam, as, sts, plan);  \
-      else e = run_batches<S, C, V, true, false, Q>(sc, cam, as, sts, plan);       \
-    } else {                                                                       \
-      if (fancy) e = run_batches<S, C, V, false, true, Q>(sc, cam, as, sts, plan); \
-      else e = run_batches<S, C, V, false, false, Q>(sc, cam, as, sts, plan);      \
-    }                                                                              \
+#define RUN3(S, C, V, E, Q)                                                          \
+  do {                                                                               \
+    if (shade == SHADE_FULL) e = run_batches<S, C, V, E, SHADE_FULL, Q>(sc, cam, as, sts, plan);        \
+    else if (shade == SHADE_MAT) e = run_batches<S, C, V, E, SHADE_MAT, Q>(sc, cam, as, sts, plan);     \
+    else e = run_batches<S, C, V, E, SHADE_LEAN, Q>(sc, cam, as, sts, plan);                            \
+  } while (0)
+#define RUN2(S, C, V, Q)            \
+  do {                              \
+    if (envis) RUN3(S, C, V, true, Q); \
+    else RUN3(S, C, V, false, Q);   \
   } while (0)
     // RT_NODES_QUANT8 scenes run the quantised-node traversal (its own kernels:
     // the default fp32 kernels carry no trace of it)
@@ -999,7 +1012,8 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     if (quant) RUN2(S, C, V, true);             \
     else RUN2(S, C, V, false);                  \
   } while (0)
-    const bool envis = sc.env.valid && sc.env.use_is, fancy = sc.has_fancy != 0, quant = sc.quant_nodes != 0;
+    const bool envis = sc.env.valid && sc.env.use_is, quant = sc.quant_nodes != 0;
+    const int shade = sc.shade_kind;
 #if defined(RTG_RING24) && !defined(RTG_DIAG_RING)
 #define RTG_DIAG_RING 24
 #endif
@@ -1022,6 +1036,7 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
 #endif
 #undef RUN
 #undef RUN2
+#undef RUN3
     if (e != hipSuccess) return e;
   }
   if (!count)

@@ -94,13 +94,13 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
   d.n_volumes = uint32_t(h.volumes.size());
   d.n_circles = uint32_t(h.circles.size());
-  d.has_fancy = 0;
+  d.shade_kind = SHADE_LEAN;   // the k_shade variant (wavefront.hip)
   for (const DMaterial& m : h.materials)
-    if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.has_fancy = 1;
+    if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.shade_kind = SHADE_MAT;
   d.needs_uv = 0;
-  for (const DTexture& t : h.textures) {   // as api.cpp rt_scene_upload
+  for (const DTexture& t : h.textures) {
     if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
-    if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.has_fancy = 1;
+    if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.shade_kind = SHADE_FULL;   // the full tex_value / make_record
   }
 
   const rt_camera_desc* c = rts_scene_get_camera(E.scn);

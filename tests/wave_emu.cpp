@@ -24,7 +24,7 @@ namespace {
 
 constexpr int kRing = 4;
 
-template <bool kVol, bool kEnvIS, bool kFancy, bool kQuant>
+template <bool kVol, bool kEnvIS, int kShade, bool kQuant>
 void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_t spb, int max_depth, float* out) {
   uint32_t* cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
   uint32_t* cnt_shadow = a.counts + CNT_SHADOW;
@@ -40,11 +40,11 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
       if (b == 0) {
         k_extend<kRing, false, kVol, true, kQuant>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
                                            fetch_ext, s0);
-        k_shade<false, kEnvIS, kFancy, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
+        k_shade<false, kEnvIS, kShade, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       } else {
         k_extend<kRing, false, kVol, false, kQuant>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
                                             fetch_ext, s0);
-        k_shade<false, kEnvIS, kFancy, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
+        k_shade<false, kEnvIS, kShade, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       }
       if (sc.num_lights > 0) {   // as run_batches: no lights, no NEE launches
         k_shadow<kRing, false, kVol, kEnvIS, kQuant>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
@@ -107,19 +107,24 @@ int main(int argc, char** argv) {
   a.slots = uint32_t(S);
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
-  const bool vol = d.has_volumes != 0 || d.n_circles > 0, envis = d.env.valid && d.env.use_is, fancy = d.has_fancy != 0;
-#define RUN(V, H, F)                                                  \
-  do {                                                                \
+  const bool vol = d.has_volumes != 0 || d.n_circles > 0, envis = d.env.valid && d.env.use_is;
+#define RUNQ(V, H, F)                                                  \
+  do {                                                                 \
     if (d.quant_nodes) run<V, H, F, true>(d, cam, a, spp, spb, E.max_depth, out.data()); \
     else run<V, H, F, false>(d, cam, a, spp, spb, E.max_depth, out.data()); \
   } while (0)
+#define RUN(V, H)                                                      \
+  do {                                                                 \
+    if (d.shade_kind == SHADE_FULL) RUNQ(V, H, SHADE_FULL);            \
+    else if (d.shade_kind == SHADE_MAT) RUNQ(V, H, SHADE_MAT);         \
+    else RUNQ(V, H, SHADE_LEAN);                                       \
+  } while (0)
   if (vol) {
-    if (envis) { if (fancy) RUN(true, true, true); else RUN(true, true, false); }
-    else { if (fancy) RUN(true, false, true); else RUN(true, false, false); }
+    if (envis) RUN(true, true); else RUN(true, false);
   } else {
-    if (envis) { if (fancy) RUN(false, true, true); else RUN(false, true, false); }
-    else { if (fancy) RUN(false, false, true); else RUN(false, false, false); }
+    if (envis) RUN(false, true); else RUN(false, false);
   }
+#undef RUNQ
 #undef RUN
   FILE* f = fopen(argv[6], "wb");
   if (!f) return 5;
