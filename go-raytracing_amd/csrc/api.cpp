@@ -858,6 +858,7 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(blas, blas);
   UP(volumes, volumes);
   UP(volume_hidx, volume_hidx);
+  UP(vol_refs, vol_refs);
   UP(materials, materials);
   UP(textures, textures);
   UP(lights, lights);
@@ -887,7 +888,6 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_materials = int(h.materials.size());
   d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed;
-  d.has_volumes = h.volumes.empty() ? 0 : 1;
   d.quant_nodes = h.quant_nodes;
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
@@ -902,6 +902,11 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
     if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
     if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.shade_kind = SHADE_FULL;   // the full tex_value / make_record
   }
+  // volumes lifted out of the world BVH (flatten: no circles, no Noise /
+  // Image textures) are tested in k_shade's volume variant
+  d.num_vol_refs = int32_t(h.vol_refs.size());
+  d.has_volumes = h.volumes.size() > h.vol_refs.size() ? 1 : 0;
+  if (d.num_vol_refs > 0) d.shade_kind = SHADE_VOL;
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;
   if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }

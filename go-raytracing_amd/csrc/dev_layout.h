@@ -232,6 +232,17 @@ struct alignas(16) DVolume {   // volume.go:9-13
   int32_t vol_id;            // RNG dimension slot
 };
 
+// A volume lifted out of the world BVH (RT scene without circles): tested
+// by k_shade on every path's ray and NEE shadow ray instead of in the
+// traversal, with what its world leaf would have given it: its TLAS ref
+// position (DFS rank, tie rule) and its leaf's test count.
+struct alignas(16) DVolRef {
+  int32_t vol;      // index into DScene.volumes
+  int32_t refpos;   // TLAS ref position (ref_rank[refpos] = its DFS rank)
+  int32_t ntests;   // Hit calls of its reference leaf (volume double test)
+  int32_t pad;
+};
+
 struct alignas(16) DMaterial {
   int32_t kind;              // rt_material_kind
   int32_t tex;
@@ -290,7 +301,7 @@ struct alignas(16) DRefBox {
 };
 
 // k_shade variants: the material / texture code a scene needs compiled in.
-enum : int32_t { SHADE_LEAN = 0, SHADE_MAT = 1, SHADE_FULL = 2 };
+enum : int32_t { SHADE_LEAN = 0, SHADE_MAT = 1, SHADE_FULL = 2, SHADE_VOL = 3 };
 
 // Everything the kernels need, passed by value as a kernel argument.
 struct DScene {
@@ -316,6 +327,7 @@ struct DScene {
   const int32_t* sphere_wref;    // per sphere: same (ITEM_WSPHERE)
   const DBvh* blas;
   const DVolume* volumes;
+  const DVolRef* vol_refs;     // volumes lifted out of the world BVH (k_shade tests them)
   const DMaterial* materials;
   const DTexture* textures;
   const DLight* lights;
@@ -339,8 +351,9 @@ struct DScene {
   int32_t num_materials;
   int32_t num_textures;
   int32_t stack_needed;
-  int32_t has_volumes;
-  int32_t shade_kind;     // SHADE_LEAN / SHADE_MAT / SHADE_FULL: the k_shade variant (shade_kind_of)
+  int32_t has_volumes;    // volumes inside the world BVH (the kVol traversal variant)
+  int32_t num_vol_refs;   // lifted volumes (vol_refs)
+  int32_t shade_kind;     // SHADE_LEAN / MAT / FULL / VOL: the k_shade variant
   int32_t needs_uv;       // an ImageTexture exists: hit records carry U/V
   int32_t quant_nodes;    // traverse the quantised DNodeQ nodes (RT_NODES_QUANT8), else DNode4
   // array lengths (bounds checks of the RTG_GUARD diagnostic build)

@@ -1132,7 +1132,22 @@ __device__ bool traverse(const DScene& sc, V3 wo, V3 wd, float time, float tmin,
   while (s == TRAV_RUNNING) s = trav_step<kAny, kCount, kVol, kQuant>(sc, T, S, cnt, err);
   if (!kAny) { best = trav_best(T, S); resolve_inst(sc, best); }
   else best = Best{};
-  if (kAny) return s == TRAV_ANYHIT;
+  if (kAny && s == TRAV_ANYHIT) return true;
+  // volumes lifted out of the world BVH (DVolRef): the same test over the
+  // same interval, competing like the traversal's candidates (accept_hit)
+  for (int v = 0; v < sc.num_vol_refs; ++v) {
+    const DVolRef vr = sc.vol_refs[v];
+    float tv = 0.0f;
+    if (!volume_hit<kCount>(sc, sc.volumes[GIX(vr.vol, sc.n_volumes, 55)], wo, wd, time, tmin, tmax, vr.ntests, key, bounce,
+                            voldom, tv, cnt))
+      continue;
+    if (kAny) return true;
+    if (best.kind == 0 || tv < best.t ||
+        (tv == best.t && tie_wins(sc, PK_VOLUME, vr.refpos, 0, best.kind, best.refpos, best.primpos))) {
+      best.t = tv; best.kind = PK_VOLUME; best.idx = vr.vol; best.inst = -1; best.refpos = vr.refpos; best.primpos = 0;
+    }
+  }
+  if (kAny) return false;
   return best.kind != 0;
 }
 

@@ -666,7 +666,16 @@ struct Flattener {
     return true;
   }
 
-  // World leaf: objects in order; planes lifted out (DFS rank kept).
+  // A volume lifted out of the world BVH: its ref (DFS rank) outside every
+  // world leaf's range, and its leaf's test count.
+  bool lift = false;
+  bool lift_volume(int g, int rank, int ntests) {
+    if (!add_object_ref(g, rank)) return false;
+    S.vol_refs.push_back(DVolRef{int32_t(S.refs.back() & REF_MASK), int32_t(S.refs.size() - 1), ntests, 0});
+    return true;
+  }
+
+  // World leaf: objects in order; planes (and lifted volumes) out, DFS rank kept.
   uint32_t tlas_leaf(const std::vector<int>& objs, int ntests, Box& box) {
     std::vector<int> ranks(objs.size());
     for (size_t i = 0; i < objs.size(); ++i) ranks[i] = rank_counter++;
@@ -684,7 +693,7 @@ struct Flattener {
         S.plane_hidx.push_back(g);
         continue;
       }
-      count++;
+      if (!(lift && h.kind == RT_VOLUME)) count++;
       // Pre-build BLASes: mixed BLAS leaves append refs, and the refs of
       // this world leaf must stay contiguous.
       int cur = h.kind == RT_VOLUME ? h.a : g;
@@ -698,7 +707,7 @@ struct Flattener {
     for (size_t i = 0; i < objs.size(); ++i) {
       int g = objs[i];
       const rt_hittable& h = H(g);
-      if (h.kind == RT_PLANE) continue;
+      if (h.kind == RT_PLANE || (lift && h.kind == RT_VOLUME)) continue;
       if (!add_object_ref(g, ranks[i])) return empty_leaf;
       if ((S.refs.back() >> REF_SHIFT) == uint32_t(PK_INSTANCE)) ninst++;
       box.merge(h.bbox);
@@ -707,6 +716,8 @@ struct Flattener {
       fail(RT_ERR_INVALID, "internal: non-contiguous world leaf refs");
       return empty_leaf;
     }
+    for (size_t i = 0; i < objs.size(); ++i)   // after the leaf's contiguous refs
+      if (lift && H(objs[i]).kind == RT_VOLUME && !lift_volume(objs[i], ranks[i], ntests)) return empty_leaf;
     if (count == 0) return empty_leaf;
     if (ninst > 8) { fail(RT_ERR_UNSUPPORTED, "more than 8 instances in one world leaf"); return empty_leaf; }
     if (ninst > max_leaf_inst) max_leaf_inst = ninst;
@@ -842,6 +853,14 @@ struct Flattener {
           (H(cur).kind == RT_LIST || H(cur).kind == RT_BVH_NODE || H(cur).kind == RT_BVH_LEAF))
         build_blas(cur);
       if (status) return empty_leaf;
+    }
+    if (lift) {
+      std::vector<TopObj> rest;
+      for (const TopObj& o : top_objs) {
+        if (H(o.g).kind == RT_VOLUME) { if (!lift_volume(o.g, o.rank, o.ntests)) return empty_leaf; }
+        else rest.push_back(o);
+      }
+      top_objs.swap(rest);
     }
     if (top_objs.empty()) return empty_leaf;
     max_leaf_inst = 1;
@@ -1185,6 +1204,13 @@ struct Flattener {
     for (int i = 0; i < d->num_hittables; ++i)
       if (d->hittables[i].kind == RT_VOLUME) vol_ids[i] = nv++;
     if (nv > 1024) { fail(RT_ERR_UNSUPPORTED, "too many volumes"); return status; }
+    // (the k_shade variant that tests lifted volumes has no Noise / Image
+    // texture code, and circles keep the rare-primitive traversal anyway)
+    bool circles = false, tex = false;
+    for (int i = 0; i < d->num_hittables; ++i) circles = circles || d->hittables[i].kind == RT_CIRCLE;
+    for (int i = 0; i < d->num_textures && d->textures; ++i)
+      tex = tex || d->textures[i].kind == RT_TEX_NOISE || d->textures[i].kind == RT_TEX_IMAGE;
+    lift = opt.lift_volumes && nv > 0 && !circles && !tex;
     for (int i = 0; i < d->num_hittables; ++i) {
       const rt_hittable& h = d->hittables[i];
       if ((is_prim(h.kind) || h.kind == RT_PLANE || h.kind == RT_VOLUME) &&

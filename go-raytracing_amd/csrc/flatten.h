@@ -39,6 +39,7 @@ struct HostScene {
   std::vector<DBvh> blas;
   std::vector<DVolume> volumes;
   std::vector<int32_t> volume_hidx;
+  std::vector<DVolRef> vol_refs;     // volumes lifted out of the world BVH (FlattenOptions::lift_volumes)
   std::vector<DMaterial> materials;
   std::vector<DTexture> textures;
   std::vector<DLight> lights;
@@ -75,6 +76,10 @@ struct FlattenOptions {
   int tlas_builder = BLAS_SAH;   // world BVH: SAH over the top-level objects, one per leaf
   int sah_min_prims = 16;   // smaller all-triangle BLASes keep the reference topology
   int quant_nodes = 0;      // RT_NODES_QUANT8: the traversal reads DNodeQ (node_quant.h)
+  // Volumes are kept out of the world BVH and tested by k_shade (DVolRef),
+  // so the traversal kernels carry no volume code; only in scenes without
+  // circles (the traversal's rare-primitive variant would carry both).
+  int lift_volumes = 1;
 };
 
 // (Re)builds S.inst_entries from refs / instances / blas headers: call after

@@ -390,8 +390,15 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
 #ifndef RTG_SHADE_MAT_WAVES
 #define RTG_SHADE_MAT_WAVES 7
 #endif
-#define RTG_SHADE_WAVES_FOR(kShade) \
-  ((kShade) == SHADE_FULL ? RTG_SHADE_WAVES : (kShade) == SHADE_MAT ? RTG_SHADE_MAT_WAVES : RTG_SHADE_LEAN_WAVES)
+// The volume variant (the material one + the lifted volumes' tests): C3
+// CornellBoxScene at 4 / 5 / 7 waves 1390 / 1454 / 1427 Msamples/s (110 / 96
+// / 72 VGPRs; 0 / 3 / 71 spilled).
+#ifndef RTG_SHADE_VOL_WAVES
+#define RTG_SHADE_VOL_WAVES 5
+#endif
+#define RTG_SHADE_WAVES_FOR(kShade)                                                       \
+  ((kShade) == SHADE_FULL ? RTG_SHADE_WAVES : (kShade) == SHADE_MAT ? RTG_SHADE_MAT_WAVES \
+   : (kShade) == SHADE_VOL ? RTG_SHADE_VOL_WAVES : RTG_SHADE_LEAN_WAVES)
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
 // and this kernel initialises the slot's radiance in Lout.
 template <bool kCount, bool kEnvIS, int kShade, bool kFirst>
@@ -489,7 +496,29 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
         beta = mk(b4.x, b4.y, b4.z);
       }
       const float time = ray_time(key);
-      const uint32_t kh = asu(h.y);
+      uint32_t kh = asu(h.y);
+      float ht = h.x;
+      int hinst = int(asu(h.z));
+      if (kShade == SHADE_VOL) {
+        // volumes lifted out of the world BVH (DVolRef): Volume.Hit
+        // (volume.go:34-79) over the ray's whole interval, as the traversal
+        // ran it, competing with k_extend's surface hit by the accept rule
+        // (closer, or on an exact tie the reference's DFS order)
+        int hrefpos = int(asu(h.w));
+        for (int v = 0; v < sc.num_vol_refs; ++v) {
+          const DVolRef vr = sc.vol_refs[v];
+          float tv = 0.0f;
+          if (!volume_hit<kCount>(sc, sc.volumes[GIX(vr.vol, sc.n_volumes, 56)], ro, rd, time, 0.001f, __builtin_inff(),
+                                  vr.ntests, key, bounce, DOM_VOL, tv, cnt))
+            continue;
+          if (kh == 0u || tv < ht || (tv == ht && tie_wins(sc, PK_VOLUME, vr.refpos, 0, int(kh >> 28), hrefpos, 0))) {
+            kh = (uint32_t(PK_VOLUME) << 28) | uint32_t(vr.vol);
+            ht = tv;
+            hinst = -1;
+            hrefpos = vr.refpos;
+          }
+        }
+      }
 #ifdef RTG_GUARD
       if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
 #endif
@@ -508,7 +537,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
         add_L(bg);
       } else {
         Best b{};
-        b.t = h.x; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = int(asu(h.z));
+        b.t = ht; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = hinst;
         b.refpos = 0; b.primpos = 0;
         Rec rec = make_record<kShade == SHADE_FULL>(sc, b, ro, rd, time);
         P = rec.P;
@@ -620,6 +649,22 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
                     flags |= 1u;
                   }
                 }
+              }
+            }
+            if (kShade == SHADE_VOL && flags != 0u) {
+              // a lifted volume occluding a shadow ray (camera.go:582, :639;
+              // the any-hit traversal's volume test, same interval and RNG
+              // domain) clears the ray: its contribution is not applied
+              for (int v = 0; v < sc.num_vol_refs; ++v) {
+                const DVolRef vr = sc.vol_refs[v];
+                const DVolume& vol = sc.volumes[GIX(vr.vol, sc.n_volumes, 57)];
+                float tv = 0.0f;
+                if ((flags & 2u) && volume_hit<kCount>(sc, vol, P, dh, 0.0f, 0.001f, __builtin_inff(), vr.ntests, key, bounce,
+                                                       DOM_VOL_SH_HDRI, tv, cnt))
+                  flags &= ~2u;
+                if ((flags & 1u) && volume_hit<kCount>(sc, vol, P, da, 0.0f, 0.001f, tmax_a, vr.ntests, key, bounce,
+                                                       DOM_VOL_SH_AREA, tv, cnt))
+                  flags &= ~1u;
               }
             }
             want_shadow = flags != 0u;
@@ -997,6 +1042,7 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
 #define RUN3(S, C, V, E, Q)                                                          \
   do {                                                                               \
     if (shade == SHADE_FULL) e = run_batches<S, C, V, E, SHADE_FULL, Q>(sc, cam, as, sts, plan);        \
+    else if (shade == SHADE_VOL) e = run_batches<S, C, V, E, SHADE_VOL, Q>(sc, cam, as, sts, plan);     \
     else if (shade == SHADE_MAT) e = run_batches<S, C, V, E, SHADE_MAT, Q>(sc, cam, as, sts, plan);     \
     else e = run_batches<S, C, V, E, SHADE_LEAN, Q>(sc, cam, as, sts, plan);                            \
   } while (0)

@@ -75,7 +75,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.tri_shade = E.tri_shade.data();
   d.leaves = pad(h.leaves); d.tris = pad(h.tris); d.quads = pad(h.quads); d.spheres = pad(h.spheres);
   d.quad_wref = ptr(h.quad_wref); d.sphere_wref = ptr(h.sphere_wref);
-  d.volumes = ptr(h.volumes); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
+  d.volumes = ptr(h.volumes); d.vol_refs = ptr(h.vol_refs); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
   d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);
   d.tri_rank = ptr(h.tri_rank); d.tlas_ref_top = ptr(h.ref_top); d.sphere_hidx = ptr(h.sphere_hidx);
   d.quad_hidx = ptr(h.quad_hidx); d.tri_hidx = ptr(h.tri_hidx); d.plane_hidx = ptr(h.plane_hidx);
@@ -87,7 +87,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.env.conditional = ptr(h.env_conditional);
   d.num_planes = int(h.planes.size()); d.num_lights = int(h.lights.size());
   d.num_materials = int(h.materials.size()); d.num_textures = int(h.textures.size());
-  d.stack_needed = h.stack_needed; d.has_volumes = h.volumes.empty() ? 0 : 1;
+  d.stack_needed = h.stack_needed;
   d.quant_nodes = h.quant_nodes;
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
@@ -102,6 +102,11 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
     if (t.kind == RT_TEX_IMAGE) d.needs_uv = 1;
     if (t.kind == RT_TEX_IMAGE || t.kind == RT_TEX_NOISE) d.shade_kind = SHADE_FULL;   // the full tex_value / make_record
   }
+  // volumes lifted out of the world BVH (flatten: no circles, no Noise /
+  // Image textures) are tested in k_shade's volume variant
+  d.num_vol_refs = int32_t(h.vol_refs.size());
+  d.has_volumes = h.volumes.size() > h.vol_refs.size() ? 1 : 0;
+  if (d.num_vol_refs > 0) d.shade_kind = SHADE_VOL;
 
   const rt_camera_desc* c = rts_scene_get_camera(E.scn);
   DCamera& cam = E.cam;

@@ -116,6 +116,7 @@ int main(int argc, char** argv) {
 #define RUN(V, H)                                                      \
   do {                                                                 \
     if (d.shade_kind == SHADE_FULL) RUNQ(V, H, SHADE_FULL);            \
+    else if (d.shade_kind == SHADE_VOL) RUNQ(V, H, SHADE_VOL);         \
     else if (d.shade_kind == SHADE_MAT) RUNQ(V, H, SHADE_MAT);         \
     else RUNQ(V, H, SHADE_LEAN);                                       \
   } while (0)
