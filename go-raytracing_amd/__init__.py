@@ -30,6 +30,8 @@ ASSET_DIR = os.path.join(REPO_DIR, "assets")
 RT_OK = 0
 RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER, RT_OPT_NODE_FORMAT = 1, 2, 3
 RT_OPT_BATCH_SLOTS, RT_OPT_REFILL, RT_OPT_MAX_BLOCKS, RT_OPT_STREAMS = 4, 5, 6, 7
+RT_OPT_VOLUMES = 8
+RT_VOLUMES_LIFTED, RT_VOLUMES_IN_BVH = 0, 1
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",

@@ -741,6 +741,11 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
     ctx->fopt.quant_nodes = value == RT_NODES_QUANT8 ? 1 : 0;
     return RT_OK;
   }
+  if (key == RT_OPT_VOLUMES) {
+    if (value != RT_VOLUMES_LIFTED && value != RT_VOLUMES_IN_BVH) return set_err(ctx, RT_ERR_INVALID, "bad volumes option");
+    ctx->fopt.lift_volumes = value == RT_VOLUMES_LIFTED ? 1 : 0;
+    return RT_OK;
+  }
   if (key == RT_OPT_BATCH_SLOTS) {
     if (value < 0) return set_err(ctx, RT_ERR_INVALID, "bad batch slots");
     ctx->opt_slots = size_t(value);

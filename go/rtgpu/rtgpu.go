@@ -93,6 +93,9 @@ const (
 	OptRefill      int32 = 5 // RT_OPT_REFILL
 	OptMaxBlocks   int32 = 6 // RT_OPT_MAX_BLOCKS
 	OptStreams     int32 = 7 // RT_OPT_STREAMS
+	OptVolumes     int32 = 8 // RT_OPT_VOLUMES
+	VolumesLifted  int32 = 0 // RT_VOLUMES_LIFTED
+	VolumesInBVH   int32 = 1 // RT_VOLUMES_IN_BVH
 	BuildReference int32 = 0 // RT_BLAS_REFERENCE
 	BuildSAH       int32 = 1 // RT_BLAS_SAH
 	BuildDevice    int32 = 2 // RT_BLAS_DEVICE
@@ -340,7 +343,7 @@ func (c *Ctx) check(rc C.int) error {
 }
 
 // SetOption sets a context option (OptBLASBuilder / OptTLASBuilder /
-// OptNodeFormat, or a schedule option: OptBatchSlots, OptRefill,
+// OptNodeFormat / OptVolumes, or a schedule option: OptBatchSlots, OptRefill,
 // OptMaxBlocks, OptStreams, which never change the image).  The scene
 // options take effect at the next Upload, the schedule options at the next
 // render.

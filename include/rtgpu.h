@@ -295,7 +295,13 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *     closest hits equal the fp32 format's only within that envelope (every
  *     BASELINE scene is inside it).  Scenes holding a RotateX/RotateZ wrapper
  *     always use RT_NODES_FP32 (their node boxes decide which rays reach
- *     an object, transform.go:201-351).                                   */
+ *     an object, transform.go:201-351).
+ *   RT_OPT_VOLUMES: RT_VOLUMES_LIFTED (default) = Volume objects are kept
+ *     out of the world BVH and tested by the shading kernel on every path
+ *     ray and NEE shadow ray (same results: the volume test runs over the
+ *     ray's whole interval and competes by the tie rule); RT_VOLUMES_IN_BVH
+ *     = tested inside the traversal.  Scenes with a Circle or a Noise /
+ *     Image texture always keep them in the BVH.                          */
 /* Schedule options (take effect at the next render; 0 = automatic).  They
  * change how the work is dealt to the GPU, never the image: the closest hit
  * is independent of the traversal schedule.
@@ -309,9 +315,11 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *     tails overlap the others' kernels; 1 keeps one stream.  Default: 3
  *     for renders of more than 2^28 samples (pixels x spp), else 2.        */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
-       RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7 };
+       RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7,
+       RT_OPT_VOLUMES = 8 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
+enum { RT_VOLUMES_LIFTED = 0, RT_VOLUMES_IN_BVH = 1 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);
 
 /* Flatten + upload the Go object graph (copied; caller memory not retained). */

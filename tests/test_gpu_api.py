@@ -150,3 +150,25 @@ def test_kernel_times_pair_twin_launches(g, ctx):
         for k in ("extend", "shade", "shadow"):
             assert t[f"{k}_launches"] == 5, (streams, k, t)
             assert t[f"{k}_ms"] > 0.0
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell-smoke"])
+def test_lifted_volumes_equal_volumes_in_bvh(g, ctx, name):
+    """RT_OPT_VOLUMES: volumes lifted out of the world BVH and tested by
+    k_shade's volume variant (closest hit by the tie rule, NEE shadow rays
+    cleared when a volume occludes them) render the same frame, bit for bit,
+    as volumes tested inside the traversal; unknown values are refused."""
+    s = g.Scene(name, width=64)
+    p = g.make_params(8, 5, seed=29)
+    frames = {}
+    try:
+        with pytest.raises(g.RTError):
+            ctx.set_option(g.RT_OPT_VOLUMES, 2)
+        for mode in (g.RT_VOLUMES_IN_BVH, g.RT_VOLUMES_LIFTED):
+            ctx.set_option(g.RT_OPT_VOLUMES, mode)
+            ctx.upload(s.desc)
+            frames[mode], _ = ctx.render(s.camera, p)
+    finally:
+        ctx.set_option(g.RT_OPT_VOLUMES, g.RT_VOLUMES_LIFTED)
+    assert np.isfinite(frames[g.RT_VOLUMES_LIFTED]).all()
+    assert np.array_equal(frames[g.RT_VOLUMES_IN_BVH], frames[g.RT_VOLUMES_LIFTED])
