@@ -18,6 +18,9 @@
 #include "flatten.h"
 
 #include <algorithm>
+#include <array>
+#include <cstdlib>
+#include <string>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -1093,12 +1096,68 @@ struct Flattener {
     if (std::isinf(dx) || std::isinf(dy) || std::isinf(dz)) return 1e300;
     return dx * dy + dy * dz + dz * dx;
   }
+  // SAH-optimal collapse (the default; RTGPU_BVH4_COLLAPSE=greedy selects the
+  // greedy one above).  Every leaf appears once in any collapse, so the
+  // collapses differ only in their BVH4 nodes, and a node costs a ray the
+  // chance of visiting it, its box's surface area.  Per BVH2 node n,
+  // dp_cost[n][k] (k = 2..4) is the least total area of the BVH4 nodes below
+  // n when n's subtree is cut into k child items, and dp_cost[n][1] that of n
+  // made one child item (its own BVH4 node + its best cut); dp_split keeps the
+  // choices (k: items from the left child; 1: the best k).  The cuts keep the
+  // left-to-right order.
+  std::vector<std::array<double, 5>> dp_cost;
+  std::vector<std::array<int8_t, 5>> dp_split;
+  std::vector<uint8_t> dp_done;
+  static bool collapse_greedy() {
+    static const bool g = [] {
+      const char* v = std::getenv("RTGPU_BVH4_COLLAPSE");
+      return v && std::string(v) == "greedy";
+    }();
+    return g;
+  }
+  double dp_item(uint32_t item, int k) {
+    if ((item >> ITEM_SHIFT) != ITEM_NODE) return k == 1 ? 0.0 : std::numeric_limits<double>::infinity();
+    dp_node(item & ITEM_MASK);
+    return dp_cost[item & ITEM_MASK][k];
+  }
+  void dp_node(uint32_t n2) {
+    if (dp_done[n2]) return;
+    const DNode nd = S.nodes[n2];
+    for (int k = 1; k <= 4; ++k) { dp_item(nd.litem, k); dp_item(nd.ritem, k); }
+    std::array<double, 5> c;
+    std::array<int8_t, 5> s{};
+    c.fill(std::numeric_limits<double>::infinity());
+    for (int k = 2; k <= 4; ++k)
+      for (int a = 1; a < k; ++a) {
+        const double v = dp_item(nd.litem, a) + dp_item(nd.ritem, k - a);
+        if (v < c[k]) { c[k] = v; s[k] = int8_t(a); }
+      }
+    float box[6];
+    for (int i = 0; i < 6; i += 2) { box[i] = std::min(nd.l[i], nd.r[i]); box[i + 1] = std::max(nd.l[i + 1], nd.r[i + 1]); }
+    int kb = 2;
+    for (int k = 3; k <= 4; ++k)
+      if (c[k] < c[kb]) kb = k;
+    c[1] = half_area(box) + c[kb];
+    s[1] = int8_t(kb);
+    dp_cost[n2] = c;
+    dp_split[n2] = s;
+    dp_done[n2] = 1;
+  }
+  struct Ch { uint32_t item; float box[6]; };
+  // the k child items of BVH2 item `item` (box `box`) by the recorded cuts
+  void dp_frontier(uint32_t item, const float* box, int k, Ch* out, int& nc) {
+    if (k == 1) { out[nc].item = item; std::copy(box, box + 6, out[nc].box); ++nc; return; }
+    const uint32_t n2 = item & ITEM_MASK;
+    const DNode& nd = S.nodes[n2];
+    const int a = dp_split[n2][k];
+    dp_frontier(nd.litem, nd.l, a, out, nc);
+    dp_frontier(nd.ritem, nd.r, k - a, out, nc);
+  }
   uint32_t collapse4(uint32_t item, int& need) {
     need = 0;
     if ((item >> ITEM_SHIFT) != ITEM_NODE) return item;
     const uint32_t n2 = item & ITEM_MASK;
     if (map4[n2] >= 0) { need = need4[map4[n2]]; return (ITEM_NODE << ITEM_SHIFT) | uint32_t(map4[n2]); }
-    struct Ch { uint32_t item; float box[6]; };
     Ch ch[4];
     int nc = 2;
     {
@@ -1106,7 +1165,15 @@ struct Flattener {
       ch[0].item = nd.litem; std::copy(nd.l, nd.l + 6, ch[0].box);
       ch[1].item = nd.ritem; std::copy(nd.r, nd.r + 6, ch[1].box);
     }
-    while (nc < 4) {
+    if (!collapse_greedy()) {
+      dp_node(n2);
+      const DNode& nd = S.nodes[n2];
+      const int k = dp_split[n2][1], a = dp_split[n2][k];
+      nc = 0;
+      dp_frontier(nd.litem, nd.l, a, ch, nc);
+      dp_frontier(nd.ritem, nd.r, k - a, ch, nc);
+    }
+    while (nc < 4 && collapse_greedy()) {
       int best = -1;
       double ba = -1.0;
       for (int c = 0; c < nc; ++c)
@@ -1150,6 +1217,9 @@ struct Flattener {
   }
   void build_bvh4() {
     map4.assign(S.nodes.size(), -1);
+    dp_cost.assign(S.nodes.size(), {});
+    dp_split.assign(S.nodes.size(), {});
+    dp_done.assign(S.nodes.size(), 0);
     S.nodes4.clear();
     need4.clear();
     int n = 0;
