@@ -32,6 +32,8 @@ RT_OPT_BLAS_BUILDER, RT_OPT_TLAS_BUILDER, RT_OPT_NODE_FORMAT = 1, 2, 3
 RT_OPT_BATCH_SLOTS, RT_OPT_REFILL, RT_OPT_MAX_BLOCKS, RT_OPT_STREAMS = 4, 5, 6, 7
 RT_OPT_VOLUMES = 8
 RT_VOLUMES_LIFTED, RT_VOLUMES_IN_BVH = 0, 1
+RT_OPT_BVH4_COLLAPSE = 9
+RT_COLLAPSE_SAH, RT_COLLAPSE_GREEDY = 0, 1
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
@@ -504,6 +506,11 @@ class Context:
         """BVH4 node records: "fp32" (default, 128 B) or "quant8" (64 B,
         8-bit child planes with a conservative margin); next upload."""
         self.set_option(RT_OPT_NODE_FORMAT, {"fp32": RT_NODES_FP32, "quant8": RT_NODES_QUANT8}[fmt])
+
+    def set_collapse(self, collapse: str):
+        """BVH2 -> BVH4 collapse: "sah" (default, least total node area) or
+        "greedy" (largest-area child first); same hits; next upload."""
+        self.set_option(RT_OPT_BVH4_COLLAPSE, {"sah": RT_COLLAPSE_SAH, "greedy": RT_COLLAPSE_GREEDY}[collapse])
 
     def set_schedule(self, batch_slots: int = 0, refill: int = 0, max_blocks: int = 0, streams: int = 0):
         """Schedule options (0 = automatic) for the next renders: path slots per

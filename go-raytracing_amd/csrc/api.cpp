@@ -746,6 +746,11 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
     ctx->fopt.lift_volumes = value == RT_VOLUMES_LIFTED ? 1 : 0;
     return RT_OK;
   }
+  if (key == RT_OPT_BVH4_COLLAPSE) {
+    if (value != RT_COLLAPSE_SAH && value != RT_COLLAPSE_GREEDY) return set_err(ctx, RT_ERR_INVALID, "bad collapse option");
+    ctx->fopt.greedy_collapse = value == RT_COLLAPSE_GREEDY ? 1 : 0;
+    return RT_OK;
+  }
   if (key == RT_OPT_BATCH_SLOTS) {
     if (value < 0) return set_err(ctx, RT_ERR_INVALID, "bad batch slots");
     ctx->opt_slots = size_t(value);

@@ -1096,8 +1096,9 @@ struct Flattener {
     if (std::isinf(dx) || std::isinf(dy) || std::isinf(dz)) return 1e300;
     return dx * dy + dy * dz + dz * dx;
   }
-  // SAH-optimal collapse (the default; RTGPU_BVH4_COLLAPSE=greedy selects the
-  // greedy one above).  Every leaf appears once in any collapse, so the
+  // SAH-optimal collapse (the default; RT_OPT_BVH4_COLLAPSE = RT_COLLAPSE_GREEDY,
+  // or RTGPU_BVH4_COLLAPSE=greedy for a whole process, selects the greedy one
+  // above).  Every leaf appears once in any collapse, so the
   // collapses differ only in their BVH4 nodes, and a node costs a ray the
   // chance of visiting it, its box's surface area.  Per BVH2 node n,
   // dp_cost[n][k] (k = 2..4) is the least total area of the BVH4 nodes below
@@ -1108,12 +1109,12 @@ struct Flattener {
   std::vector<std::array<double, 5>> dp_cost;
   std::vector<std::array<int8_t, 5>> dp_split;
   std::vector<uint8_t> dp_done;
-  static bool collapse_greedy() {
-    static const bool g = [] {
+  bool collapse_greedy() const {
+    static const bool env = [] {
       const char* v = std::getenv("RTGPU_BVH4_COLLAPSE");
       return v && std::string(v) == "greedy";
     }();
-    return g;
+    return env || opt.greedy_collapse != 0;
   }
   double dp_item(uint32_t item, int k) {
     if ((item >> ITEM_SHIFT) != ITEM_NODE) return k == 1 ? 0.0 : std::numeric_limits<double>::infinity();

@@ -80,6 +80,9 @@ struct FlattenOptions {
   // so the traversal kernels carry no volume code; only in scenes without
   // circles (the traversal's rare-primitive variant would carry both).
   int lift_volumes = 1;
+  // RT_OPT_BVH4_COLLAPSE: 0 = SAH-optimal BVH2 -> BVH4 collapse, 1 = greedy
+  // (open the largest-area internal child); the hits are the same
+  int greedy_collapse = 0;
 };
 
 // (Re)builds S.inst_entries from refs / instances / blas headers: call after

@@ -86,21 +86,24 @@ const (
 
 // Context options (rt_ctx_set_option).
 const (
-	OptBLASBuilder int32 = 1 // RT_OPT_BLAS_BUILDER
-	OptTLASBuilder int32 = 2 // RT_OPT_TLAS_BUILDER
-	OptNodeFormat  int32 = 3 // RT_OPT_NODE_FORMAT
-	OptBatchSlots  int32 = 4 // RT_OPT_BATCH_SLOTS
-	OptRefill      int32 = 5 // RT_OPT_REFILL
-	OptMaxBlocks   int32 = 6 // RT_OPT_MAX_BLOCKS
-	OptStreams     int32 = 7 // RT_OPT_STREAMS
-	OptVolumes     int32 = 8 // RT_OPT_VOLUMES
-	VolumesLifted  int32 = 0 // RT_VOLUMES_LIFTED
-	VolumesInBVH   int32 = 1 // RT_VOLUMES_IN_BVH
-	BuildReference int32 = 0 // RT_BLAS_REFERENCE
-	BuildSAH       int32 = 1 // RT_BLAS_SAH
-	BuildDevice    int32 = 2 // RT_BLAS_DEVICE
-	NodesFP32      int32 = 0 // RT_NODES_FP32
-	NodesQuant8    int32 = 1 // RT_NODES_QUANT8
+	OptBLASBuilder  int32 = 1 // RT_OPT_BLAS_BUILDER
+	OptTLASBuilder  int32 = 2 // RT_OPT_TLAS_BUILDER
+	OptNodeFormat   int32 = 3 // RT_OPT_NODE_FORMAT
+	OptBatchSlots   int32 = 4 // RT_OPT_BATCH_SLOTS
+	OptRefill       int32 = 5 // RT_OPT_REFILL
+	OptMaxBlocks    int32 = 6 // RT_OPT_MAX_BLOCKS
+	OptStreams      int32 = 7 // RT_OPT_STREAMS
+	OptVolumes      int32 = 8 // RT_OPT_VOLUMES
+	VolumesLifted   int32 = 0 // RT_VOLUMES_LIFTED
+	VolumesInBVH    int32 = 1 // RT_VOLUMES_IN_BVH
+	OptBVH4Collapse int32 = 9 // RT_OPT_BVH4_COLLAPSE
+	CollapseSAH     int32 = 0 // RT_COLLAPSE_SAH
+	CollapseGreedy  int32 = 1 // RT_COLLAPSE_GREEDY
+	BuildReference  int32 = 0 // RT_BLAS_REFERENCE
+	BuildSAH        int32 = 1 // RT_BLAS_SAH
+	BuildDevice     int32 = 2 // RT_BLAS_DEVICE
+	NodesFP32       int32 = 0 // RT_NODES_FP32
+	NodesQuant8     int32 = 1 // RT_NODES_QUANT8
 )
 
 // Node mirrors rt_hittable: one node per concrete rt.Hittable.  P holds the
@@ -343,7 +346,7 @@ func (c *Ctx) check(rc C.int) error {
 }
 
 // SetOption sets a context option (OptBLASBuilder / OptTLASBuilder /
-// OptNodeFormat / OptVolumes, or a schedule option: OptBatchSlots, OptRefill,
+// OptNodeFormat / OptVolumes / OptBVH4Collapse, or a schedule option: OptBatchSlots, OptRefill,
 // OptMaxBlocks, OptStreams, which never change the image).  The scene
 // options take effect at the next Upload, the schedule options at the next
 // render.

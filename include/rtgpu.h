@@ -301,7 +301,12 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *     ray and NEE shadow ray (same results: the volume test runs over the
  *     ray's whole interval and competes by the tie rule); RT_VOLUMES_IN_BVH
  *     = tested inside the traversal.  Scenes with a Circle or a Noise /
- *     Image texture always keep them in the BVH.                          */
+ *     Image texture always keep them in the BVH.
+ *   RT_OPT_BVH4_COLLAPSE: how the binary BVHs become the 4-wide nodes the
+ *     device traverses: RT_COLLAPSE_SAH (default) = the cut of each subtree
+ *     into at most four child items with the least total node surface area
+ *     (a dynamic programme); RT_COLLAPSE_GREEDY = open the largest-area
+ *     internal child until four items are held.  Same hits either way.   */
 /* Schedule options (take effect at the next render; 0 = automatic).  They
  * change how the work is dealt to the GPU, never the image: the closest hit
  * is independent of the traversal schedule.
@@ -316,10 +321,11 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *     for renders of more than 2^28 samples (pixels x spp), else 2.        */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7,
-       RT_OPT_VOLUMES = 8 };
+       RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
 enum { RT_VOLUMES_LIFTED = 0, RT_VOLUMES_IN_BVH = 1 };
+enum { RT_COLLAPSE_SAH = 0, RT_COLLAPSE_GREEDY = 1 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);
 
 /* Flatten + upload the Go object graph (copied; caller memory not retained). */

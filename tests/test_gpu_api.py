@@ -172,3 +172,27 @@ def test_lifted_volumes_equal_volumes_in_bvh(g, ctx, name):
         ctx.set_option(g.RT_OPT_VOLUMES, g.RT_VOLUMES_LIFTED)
     assert np.isfinite(frames[g.RT_VOLUMES_LIFTED]).all()
     assert np.array_equal(frames[g.RT_VOLUMES_IN_BVH], frames[g.RT_VOLUMES_LIFTED])
+
+
+@pytest.mark.parametrize("name", ["cornell-lucy", "cornell", "random"])
+def test_collapse_option_same_frame(g, ctx, name):
+    """RT_OPT_BVH4_COLLAPSE: the SAH-optimal collapse (default) uploads fewer
+    BVH4 nodes than the greedy one (or as many) and renders the same frame,
+    bit for bit (the closest hit does not depend on the node topology);
+    unknown values are refused."""
+    s = g.Scene(name, width=64, **(dict(lucy_rings=60, lucy_cols=80) if name == "cornell-lucy" else {}))
+    p = g.make_params(8, 5, seed=31)
+    frames, nodes = {}, {}
+    try:
+        with pytest.raises(g.RTError):
+            ctx.set_option(g.RT_OPT_BVH4_COLLAPSE, 2)
+        for mode in (g.RT_COLLAPSE_GREEDY, g.RT_COLLAPSE_SAH):
+            ctx.set_option(g.RT_OPT_BVH4_COLLAPSE, mode)
+            ctx.upload(s.desc)
+            nodes[mode] = ctx.info().nodes
+            frames[mode], _ = ctx.render(s.camera, p)
+    finally:
+        ctx.set_option(g.RT_OPT_BVH4_COLLAPSE, g.RT_COLLAPSE_SAH)
+    assert nodes[g.RT_COLLAPSE_SAH] <= nodes[g.RT_COLLAPSE_GREEDY]
+    assert np.isfinite(frames[g.RT_COLLAPSE_SAH]).all()
+    assert np.array_equal(frames[g.RT_COLLAPSE_GREEDY], frames[g.RT_COLLAPSE_SAH])

@@ -56,18 +56,21 @@ def test_primary_hits_bit_exact(g, O, ctx, name, kw):
         assert (tg >= 0).any()
 
 
+@pytest.mark.parametrize("collapse", ["sah", "greedy"])
 @pytest.mark.parametrize("builder", ["reference", "sah", "device"])
 @pytest.mark.parametrize("name", ["cornell-lucy", "random", "cornell-smoke"])
-def test_bvh_builders_same_hits(g, O, builder, name):
+def test_bvh_builders_same_hits(g, O, builder, name, collapse):
     """The SAH BVHs (mesh BLAS, world), the device-built LBVH mesh BLAS and the
-    reference topology give the same first hits (ids and t) as the oracle,
-    which walks the caller's graph."""
+    reference topology, each collapsed to BVH4 nodes either way
+    (RT_OPT_BVH4_COLLAPSE), give the same first hits (ids and t) as the
+    oracle, which walks the caller's graph."""
     s = _scene(g, name, dict(width=64, **LUCY) if name == "cornell-lucy" else dict(width=64))
     cam = s.camera
     c = g.Context(0)
     try:
         c.set_blas_builder(builder)
         c.set_tlas_builder("sah" if builder == "device" else builder)
+        c.set_collapse(collapse)
         c.upload(s.desc)
         tg, pg, t_g = c.primary_hits(cam, 99, 1)
         to, po, t_o = O.primary_hits(s.desc, cam, 99, 1, fp32=True)
