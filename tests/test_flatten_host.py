@@ -59,9 +59,13 @@ def _env():
     return env
 
 
+@pytest.mark.parametrize("collapse", ["sah", "greedy"])
 @pytest.mark.parametrize("name", SCENES)
-def test_flattened_indices_in_range(probe, name):
-    r = subprocess.run([probe, name, "64", ASSETS], capture_output=True, text=True)
+def test_flattened_indices_in_range(probe, name, collapse):
+    """Every index the kernels dereference is in range and the stack bound
+    holds, under both BVH2 -> BVH4 collapses (RTGPU_BVH4_COLLAPSE)."""
+    env = dict(os.environ, RTGPU_BVH4_COLLAPSE=collapse)
+    r = subprocess.run([probe, name, "64", ASSETS], capture_output=True, text=True, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     info = json.loads(r.stdout)
     assert info["fails"] == 0, info
