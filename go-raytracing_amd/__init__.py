@@ -194,6 +194,10 @@ def rtgpu() -> C.CDLL:
         if hasattr(lib, "rt_extend_first_hits"):
             lib.rt_extend_first_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, C.POINTER(I32),
                                                  C.POINTER(I32), C.POINTER(C.c_float)]
+        if hasattr(lib, "rt_extend_hits"):
+            lib.rt_extend_hits.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, I32, C.POINTER(I32), C.POINTER(I32),
+                                           C.POINTER(C.c_float), C.POINTER(C.c_float)]
+            lib.rt_shadow_visibility.argtypes = [P, C.POINTER(RtCameraDesc), U32, I32, I32, C.POINTER(I32)]
         _rtgpu = lib
     return _rtgpu
 
@@ -556,6 +560,27 @@ class Context:
         self._check(self._lib.rt_extend_first_hits(self._h, C.byref(camera), seed, sample, _i32p(top), _i32p(prim),
                                                    _f32p(t)))
         return top, prim, t
+
+    def extend_hits(self, camera: RtCameraDesc, seed: int, sample: int, bounce: int):
+        """Closest hit of every pixel's bounce-`bounce` ray from the production
+        k_extend (rt_extend_hits): top, prim (-1 miss, -2 path ended), t, and
+        the incoming ray (n, 6) float32 (origin, direction)."""
+        n = camera.image_width * camera.image_height
+        top = np.zeros(n, np.int32)
+        prim = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        ray = np.zeros((n, 6), np.float32)
+        self._check(self._lib.rt_extend_hits(self._h, C.byref(camera), seed, sample, bounce, _i32p(top), _i32p(prim),
+                                             _f32p(t), _f32p(ray)))
+        return top, prim, t, ray
+
+    def shadow_visibility(self, camera: RtCameraDesc, seed: int, sample: int, bounce: int) -> np.ndarray:
+        """NEE shadow rays of bounce `bounce` per pixel (rt_shadow_visibility):
+        bits 0/1 area/HDRI ray traced, bits 2/3 unoccluded."""
+        n = camera.image_width * camera.image_height
+        nee = np.zeros(n, np.int32)
+        self._check(self._lib.rt_shadow_visibility(self._h, C.byref(camera), seed, sample, bounce, _i32p(nee)))
+        return nee
 
 
 # ---------------------------------------------------------------------------

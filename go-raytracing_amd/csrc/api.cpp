@@ -74,9 +74,8 @@ struct rt_ctx {
   hipStream_t twin_st[kMaxTwins - 1] = {};   // twins 1.. (twin 0 runs on the caller's stream)
   hipEvent_t twin_ev0 = nullptr, twin_end[kMaxTwins - 1] = {};
   int num_twins = 1;
-  const float4* twin_hit[kMaxTwins] = {};
-  const uint32_t* twin_pix[kMaxTwins] = {};
-  uint32_t twin_npix[kMaxTwins] = {};
+  WaveArgs twin_args[kMaxTwins] = {};   // each twin's buffers (the path probes read them)
+  int bounces_run = 0;                  // bounces the last render's last batch ran (WavePlan::bounces_run)
   // device BVH build (RT_BLAS_DEVICE) of the last upload
   uint32_t dev_nodes = 0, dev_leaves = 0;   // nodes / leaves added on the device
   double build_ms = 0.0;                    // wall time of the device builds
@@ -322,12 +321,17 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   const uint32_t spb = (spp + nbatch - 1) / nbatch;
   const size_t nslots = size_t(spb) * npix;   // over both twins
   int rc;
+  // Every twin takes kSlotF4 float4 arrays of its S_t slots and, in `wq`, its
+  // CNT_WORDS_Q queue counters plus two job words per slot: room for
+  // kMaxTwins twins' counters whatever `nt` this render uses (S_t sum to
+  // nslots over the twins).
+  const size_t wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
   if (ctx->wslots < nslots) {
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
     ctx->wslots = 0;
     if ((rc = ensure(ctx, ctx->wstate, nslots * size_t(kSlotF4) * sizeof(float4)))) return rc;
-    if ((rc = ensure(ctx, ctx->wq, nslots * 2 * sizeof(uint32_t) + 2 * CNT_WORDS_Q * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(ctx, ctx->wq, wq_bytes))) return rc;
     ctx->wslots = nslots;
   }
   if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
@@ -407,10 +411,14 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     a.spill_cap = spill_cap;
     a.spill = static_cast<uint32_t*>(ctx->wspill.p) + size_t(t) * spill_words;
     a.slots = uint32_t(S);
-    ctx->twin_hit[t] = a.hit;
-    ctx->twin_pix[t] = a.pixels;
-    ctx->twin_npix[t] = a.npix;
+    ctx->twin_args[t] = a;
   }
+  // the twins' slices must lie inside the batch buffers (an internal error
+  // otherwise: nothing is launched)
+  const size_t f4_used = size_t(fbase - static_cast<float4*>(ctx->wstate.p)) * sizeof(float4);
+  const size_t q_used = size_t(qbase - static_cast<uint32_t*>(ctx->wq.p)) * sizeof(uint32_t);
+  if (f4_used > ctx->wstate.bytes || q_used > ctx->wq.bytes || q_used > wq_bytes)
+    return set_err(ctx, RT_ERR_INVALID, "internal: twin buffers exceed the batch allocation");
   ctx->num_twins = nt;
   WavePlan plan{};
   plan.spp = spp;
@@ -436,6 +444,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   }();
   plan.debug_sync = debug_sync;
   plan.probe_host = ctx->probe_pinned;
+  plan.bounces_run = &ctx->bounces_run;
   ctx->tev_used = 0;
   if (ctx->timing) {
     // worst case: 2 events per timed launch, 3 timed launches per bounce, per batch and twin
@@ -1201,8 +1210,12 @@ int rt_render_rgba8(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_para
   if (!bk.empty()) {   // quantise the rendered buckets on the device (bucket_renderer.go:276-285)
     if ((rc = ensure(ctx, ctx->frame_buckets, bk.size() * sizeof(int4)))) return rc;
     HIPCHK(hipMemcpyAsync(ctx->frame_buckets.p, bk.data(), bk.size() * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(launch_tonemap_buckets(fr, W, static_cast<const int4*>(ctx->frame_buckets.p), int(bk.size()),
-                                  params->samples_per_pixel, static_cast<uint8_t*>(ctx->frame_rgba.p), ctx->stream));
+    // the sums hold samples [0, sample_offset + spp) after an accumulating
+    // pass that continues the earlier ones, samples [offset, offset + spp)
+    // after an overwriting one
+    const int32_t nsum = params->accumulate ? params->sample_offset + params->samples_per_pixel : params->samples_per_pixel;
+    HIPCHK(launch_tonemap_buckets(fr, W, static_cast<const int4*>(ctx->frame_buckets.p), int(bk.size()), nsum,
+                                  static_cast<uint8_t*>(ctx->frame_rgba.p), ctx->stream));
   }
   HIPCHK(hipMemcpyAsync(rgba_out, ctx->frame_rgba.p, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1253,30 +1266,78 @@ int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32
   return RT_OK;
 }
 
-int rt_extend_first_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t* out_top,
-                         int32_t* out_prim, float* out_t) {
-  if (!ctx || !cam || !out_top || !out_prim || !out_t || sample < 0) return RT_ERR_INVALID;
+}  // extern "C"
+
+namespace {
+// The path probes: one sample of every pixel rendered by the production
+// pipeline to depth bounce + 1 (the rays of bounce k do not depend on the
+// depth beyond it: the RNG is keyed by bounce, camera.go:443-518 decides
+// nothing by the remaining depth but the phantom HDRI of the camera ray), so
+// the records of bounce `bounce` are the last the pipeline wrote: k_extend's
+// hit records and the stream it traced, and the NEE jobs with k_shadow's
+// visibility words.  `what`: 1 = hits (+ ray), 2 = NEE.  Multi-device
+// contexts probe their first device.
+int path_probe(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t bounce, int what,
+               int32_t* out_top, int32_t* out_prim, float* out_t, float* out_ray, int32_t* out_nee) {
+  if (!ctx || !cam || sample < 0 || bounce < 0 || bounce > 0x7FFF) return RT_ERR_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(ctx, RT_ERR_INVALID, "bad image size");
-  const size_t n = size_t(cam->image_width) * cam->image_height;
-  int rc = ensure(ctx, ctx->accum, n * 3 * sizeof(float));
+  if (!ctx->has_scene) return set_err(ctx, RT_ERR_NO_SCENE, "no scene uploaded");
+  DCamera dc{};
+  int rc = make_camera(ctx, cam, dc);
   if (rc) return rc;
-  if ((rc = ensure(ctx, ctx->probe, n * 12))) return rc;
-  // one sample of every pixel, one bounce: the hit records of the first
-  // k_extend stay in the hit array (slot i = pixel list entry i)
-  const rt_render_params p{1, 1, sample, seed, nullptr, 0, 0};
+  const size_t n = size_t(cam->image_width) * cam->image_height;
+  if ((rc = ensure(ctx, ctx->accum, n * 3 * sizeof(float)))) return rc;
+  if ((rc = ensure(ctx, ctx->probe, n * 40))) return rc;
+  const rt_render_params p{1, bounce + 1, sample, seed, nullptr, 0, 0};
   rc = render_impl(ctx, cam, &p, static_cast<float*>(ctx->accum.p), ctx->stream, false, nullptr, nullptr);
   if (rc) return rc;
   int32_t* top = static_cast<int32_t*>(ctx->probe.p);
   int32_t* prim = top + n;
   float* t = reinterpret_cast<float*>(prim + n);
-  for (int k = 0; k < ctx->num_twins; ++k)   // each twin's hit records (render_wave)
-    HIPCHK(launch_hit_ids(ctx->dscene, ctx->twin_hit[k], ctx->twin_pix[k], ctx->twin_npix[k], top, prim, t, ctx->stream));
-  HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  float* ray = t + n;
+  int32_t* nee = reinterpret_cast<int32_t*>(ray + 6 * n);
+  HIPCHK(launch_path_fill(uint32_t(n), top, prim, t, ray, nee, ctx->stream));
+  // the long-tail early exit (run_batches) may have ended the render before
+  // this bounce: then every path had ended and the fill values stand
+  if (ctx->bounces_run > bounce) {
+    for (int k = 0; k < ctx->num_twins; ++k) {   // each twin's records (render_wave)
+      const WaveArgs& a = ctx->twin_args[k];
+      const int c = bounce & 1;
+      if (what & 1)
+        HIPCHK(launch_path_hits(ctx->dscene, dc, a.hit, a.s[c].o, a.s[c].d, a.counts + (c ? CNT_STREAM1 : CNT_STREAM0),
+                                a.pixels, a.npix, seed, uint32_t(sample), bounce, top, prim, t, ray, ctx->stream));
+      if (what & 2)
+        HIPCHK(launch_nee_probe(a.sj_info, a.sj_vis, a.ne_a, a.counts + CNT_SHADOW, a.pixels, a.npix, nee, ctx->stream));
+    }
+  }
+  if (out_top) HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_prim) HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_t) HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_ray) HIPCHK(hipMemcpyAsync(out_ray, ray, n * 24, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_nee) HIPCHK(hipMemcpyAsync(out_nee, nee, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return check_render_error(ctx, true);
+}
+}  // namespace
+
+extern "C" {
+
+int rt_extend_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t bounce,
+                   int32_t* out_top, int32_t* out_prim, float* out_t, float* out_ray) {
+  if (!out_top || !out_prim || !out_t) return RT_ERR_INVALID;
+  return path_probe(ctx, cam, seed, sample, bounce, 1, out_top, out_prim, out_t, out_ray, nullptr);
+}
+
+int rt_shadow_visibility(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t bounce,
+                         int32_t* out_nee) {
+  if (!out_nee) return RT_ERR_INVALID;
+  return path_probe(ctx, cam, seed, sample, bounce, 2, nullptr, nullptr, nullptr, nullptr, out_nee);
+}
+
+int rt_extend_first_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t* out_top,
+                         int32_t* out_prim, float* out_t) {
+  return rt_extend_hits(ctx, cam, seed, sample, 0, out_top, out_prim, out_t, nullptr);
 }
 
 }  // extern "C"

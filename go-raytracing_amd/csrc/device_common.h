@@ -509,6 +509,30 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
   return true;
 }
 
+// Volumes lifted out of the world BVH (DVolRef): Volume.Hit (volume.go:34-79)
+// over the closest-hit ray's whole interval, as the traversal ran it,
+// competing with the traversal's surface hit (kh = kind << 28 | index, 0 =
+// miss; ht; instance; TLAS ref position) by the accept rule: closer, or on an
+// exact tie the reference's DFS order.  k_shade's volume variant and the
+// path probe (probe.hip) both call this.
+template <bool kCount>
+__device__ __forceinline__ void lifted_volumes(const DScene& sc, V3 ro, V3 rd, float time, uint32_t key, uint32_t bounce,
+                                               uint32_t& kh, float& ht, int& hinst, int& hrefpos, Cnt& cnt) {
+  for (int v = 0; v < sc.num_vol_refs; ++v) {
+    const DVolRef vr = sc.vol_refs[v];
+    float tv = 0.0f;
+    if (!volume_hit<kCount>(sc, sc.volumes[GIX(vr.vol, sc.n_volumes, 56)], ro, rd, time, 0.001f, __builtin_inff(),
+                            vr.ntests, key, bounce, DOM_VOL, tv, cnt))
+      continue;
+    if (kh == 0u || tv < ht || (tv == ht && tie_wins(sc, PK_VOLUME, vr.refpos, 0, int(kh >> 28), hrefpos, 0))) {
+      kh = (uint32_t(PK_VOLUME) << 28) | uint32_t(vr.vol);
+      ht = tv;
+      hinst = -1;
+      hrefpos = vr.refpos;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------
 // BVH traversal ("while-while", Aila & Laine 2009, adapted to wave64): one
 // loop for the world BVH and instance BLASes (ray switched to object space on

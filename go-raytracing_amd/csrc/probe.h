@@ -12,8 +12,16 @@ hipError_t launch_tonemap_buckets(const float* accum, int width, const int4* buc
                                   hipStream_t st);
 hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, int sample, int32_t* top,
                           int32_t* prim, float* t, int* err, int stack, hipStream_t st);
-// Hit records of a first-bounce k_extend (slot i = pixels[i]) -> ids per pixel.
-hipError_t launch_hit_ids(const DScene& sc, const float4* hit, const uint32_t* pixels, uint32_t npix, int32_t* top,
-                          int32_t* prim, float* t, hipStream_t st);
+// Path probes (one sample per pixel, probe.hip): fill the per-pixel outputs,
+// then one twin's bounce records -> ids / t / incoming ray per pixel, and its
+// NEE jobs -> traced | visible << 2 per pixel.
+hipError_t launch_path_fill(uint32_t n, int32_t* top, int32_t* prim, float* t, float* ray, int32_t* nee,
+                            hipStream_t st);
+hipError_t launch_path_hits(const DScene& sc, const DCamera& cam, const float4* hit, const float4* so, const float4* sd,
+                            const uint32_t* count, const uint32_t* pixels, uint32_t npix, uint32_t seed,
+                            uint32_t sample, int bounce, int32_t* top, int32_t* prim, float* t, float* ray,
+                            hipStream_t st);
+hipError_t launch_nee_probe(const uint32_t* sj_info, const uint32_t* sj_vis, const float4* ne_a, const uint32_t* count,
+                            const uint32_t* pixels, uint32_t npix, int32_t* nee, hipStream_t st);
 
 }  // namespace rtg

@@ -70,21 +70,76 @@ __global__ __launch_bounds__(256) void tonemap_buckets_kernel(const float* accum
   }
 }
 
-// rt_extend_first_hits: k_extend's hit records (wavefront.hip store_hit:
-// t, kind<<28|idx, instance, refpos) of the pixel list -> ids per pixel.
-__global__ __launch_bounds__(256) void hit_ids_kernel(DScene sc, const float4* hit, const uint32_t* pixels,
-                                                      uint32_t npix, int32_t* out_top, int32_t* out_prim,
-                                                      float* out_t) {
+// Path probes (rt_extend_hits / rt_shadow_visibility): one sample per pixel
+// rendered to depth bounce + 1, so the records of bounce `bounce` are the
+// last the pipeline wrote.  Pixels whose path ended before that bounce keep
+// the fill values (ids -2, t -1, ray 0, no NEE rays).
+__global__ __launch_bounds__(256) void path_fill_kernel(uint32_t n, int32_t* top, int32_t* prim, float* t, float* ray,
+                                                        int32_t* nee) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i >= npix) return;
+  if (i >= n) return;
+  top[i] = -2;
+  prim[i] = -2;
+  t[i] = -1.0f;
+  for (int k = 0; k < 6; ++k) ray[size_t(i) * 6 + k] = 0.0f;
+  nee[i] = 0;
+}
+
+// k_extend's hit records of one bounce (wavefront.hip store_hit: t,
+// kind<<28|idx, instance, TLAS ref position; stream position i < *count)
+// -> hittable ids per pixel, with the lifted volumes' test applied as
+// k_shade applies it (lifted_volumes), and the incoming ray: bounce 0
+// regenerates the camera ray (slot i = pixel list entry i), later bounces
+// read it from the stream k_extend traced (o.w = slot, d.w = path key).
+__global__ __launch_bounds__(256) void path_hits_kernel(DScene sc, DCamera cam, const float4* hit, const float4* so,
+                                                        const float4* sd, const uint32_t* count,
+                                                        const uint32_t* pixels, uint32_t npix, uint32_t seed,
+                                                        uint32_t sample, int bounce, int32_t* out_top,
+                                                        int32_t* out_prim, float* out_t, float* out_ray) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= npix || i >= *count) return;   // one sample per pixel: at most npix paths
+  uint32_t slot, key;
+  V3 ro, rd;
+  if (bounce == 0) {
+    slot = i;
+    const uint32_t pix = pixels[i];
+    key = path_key(seed, pix, sample);
+    float tm;
+    get_ray(cam, int(pix % uint32_t(cam.width)), int(pix / uint32_t(cam.width)), key, ro, rd, tm);
+  } else {
+    const float4 o4 = so[i], d4 = sd[i];
+    slot = __float_as_uint(o4.w);
+    key = __float_as_uint(d4.w);
+    ro = mk(o4.x, o4.y, o4.z);
+    rd = mk(d4.x, d4.y, d4.z);
+  }
   const float4 h = hit[i];
-  const uint32_t kh = __float_as_uint(h.y);
+  uint32_t kh = __float_as_uint(h.y);
+  float ht = h.x;
+  int hinst = int(__float_as_uint(h.z)), hrefpos = int(__float_as_uint(h.w));
+  Cnt cnt = {};
+  if (sc.num_vol_refs > 0) lifted_volumes<false>(sc, ro, rd, ray_time(key), key, uint32_t(bounce), kh, ht, hinst, hrefpos, cnt);
   int top = -1, prim = -1;
-  if (kh != 0u) hit_ids(sc, int(kh >> 28), int(kh & 0x0FFFFFFFu), int(__float_as_uint(h.w)), top, prim);
-  const uint32_t p = pixels[i];
+  if (kh != 0u) hit_ids(sc, int(kh >> 28), int(kh & 0x0FFFFFFFu), hrefpos, top, prim);
+  const uint32_t p = pixels[slot % npix];
   out_top[p] = top;
   out_prim[p] = prim;
-  out_t[p] = kh ? h.x : -1.0f;
+  out_t[p] = kh ? ht : -1.0f;
+  float* r = out_ray + size_t(p) * 6;
+  r[0] = ro.x; r[1] = ro.y; r[2] = ro.z; r[3] = rd.x; r[4] = rd.y; r[5] = rd.z;
+}
+
+// The NEE jobs of one bounce (job j < *count): the shadow rays k_shade set
+// up (sj_info bits 0 / 1: area-light / HDRI ray; a lifted volume that
+// occludes a ray has already cleared its bit) and what k_shadow found
+// (sj_vis bits: unoccluded) -> flags | vis << 2 per pixel.
+__global__ __launch_bounds__(256) void nee_probe_kernel(const uint32_t* sj_info, const uint32_t* sj_vis,
+                                                        const float4* ne_a, const uint32_t* count,
+                                                        const uint32_t* pixels, uint32_t npix, int32_t* out_nee) {
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= npix || j >= *count) return;
+  const uint32_t slot = __float_as_uint(ne_a[j].w);
+  out_nee[pixels[slot % npix]] = int32_t((sj_info[j] & 3u) | ((sj_vis[j] & 3u) << 2));
 }
 
 // Parity probe: first-bounce closest hit of one sample per pixel.
@@ -141,11 +196,28 @@ hipError_t launch_tonemap_buckets(const float* accum, int width, const int4* buc
   return hipGetLastError();
 }
 
-hipError_t launch_hit_ids(const DScene& sc, const float4* hit, const uint32_t* pixels, uint32_t npix, int32_t* top,
-                          int32_t* prim, float* t, hipStream_t st) {
+hipError_t launch_path_fill(uint32_t n, int32_t* top, int32_t* prim, float* t, float* ray, int32_t* nee,
+                            hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(path_fill_kernel, dim3((n + 255u) / 256u), dim3(256), 0, st, n, top, prim, t, ray, nee);
+  return hipGetLastError();
+}
+
+hipError_t launch_path_hits(const DScene& sc, const DCamera& cam, const float4* hit, const float4* so, const float4* sd,
+                            const uint32_t* count, const uint32_t* pixels, uint32_t npix, uint32_t seed,
+                            uint32_t sample, int bounce, int32_t* top, int32_t* prim, float* t, float* ray,
+                            hipStream_t st) {
   if (npix == 0) return hipSuccess;
-  hipLaunchKernelGGL(hit_ids_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, st, sc, hit, pixels, npix, top, prim,
-                     t);
+  hipLaunchKernelGGL(path_hits_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, st, sc, cam, hit, so, sd, count, pixels,
+                     npix, seed, sample, bounce, top, prim, t, ray);
+  return hipGetLastError();
+}
+
+hipError_t launch_nee_probe(const uint32_t* sj_info, const uint32_t* sj_vis, const float4* ne_a, const uint32_t* count,
+                            const uint32_t* pixels, uint32_t npix, int32_t* nee, hipStream_t st) {
+  if (npix == 0) return hipSuccess;
+  hipLaunchKernelGGL(nee_probe_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, st, sj_info, sj_vis, ne_a, count,
+                     pixels, npix, nee);
   return hipGetLastError();
 }
 

@@ -73,6 +73,7 @@ struct WavePlan {
   int32_t debug_sync;       // RTGPU_DEBUG_SYNC=1: synchronise after every launch, name a failing kernel
   int32_t num_twins;        // 1..kMaxTwins parts of the pixel list on their own streams (run_batches)
   uint32_t* probe_host;     // pinned words (one per twin) for the long-tail early exit
+  int* bounces_run;         // out (may be null): bounces the last batch ran (< max_depth after the early exit)
   // Per-launch timing (rt_set_kernel_timing): events 2k and 2k+1 are
   // recorded before and after one extend / shade / shadow launch on its
   // stream; ev_class[2k] names the kernel (low 4 bits, KC_*) and the twin

@@ -500,24 +500,8 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
       float ht = h.x;
       int hinst = int(asu(h.z));
       if (kShade == SHADE_VOL) {
-        // volumes lifted out of the world BVH (DVolRef): Volume.Hit
-        // (volume.go:34-79) over the ray's whole interval, as the traversal
-        // ran it, competing with k_extend's surface hit by the accept rule
-        // (closer, or on an exact tie the reference's DFS order)
         int hrefpos = int(asu(h.w));
-        for (int v = 0; v < sc.num_vol_refs; ++v) {
-          const DVolRef vr = sc.vol_refs[v];
-          float tv = 0.0f;
-          if (!volume_hit<kCount>(sc, sc.volumes[GIX(vr.vol, sc.n_volumes, 56)], ro, rd, time, 0.001f, __builtin_inff(),
-                                  vr.ntests, key, bounce, DOM_VOL, tv, cnt))
-            continue;
-          if (kh == 0u || tv < ht || (tv == ht && tie_wins(sc, PK_VOLUME, vr.refpos, 0, int(kh >> 28), hrefpos, 0))) {
-            kh = (uint32_t(PK_VOLUME) << 28) | uint32_t(vr.vol);
-            ht = tv;
-            hinst = -1;
-            hrefpos = vr.refpos;
-          }
-        }
+        lifted_volumes<kCount>(sc, ro, rd, time, key, bounce, kh, ht, hinst, hrefpos, cnt);
       }
 #ifdef RTG_GUARD
       if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
@@ -944,8 +928,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
       gext0[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, true, kQuant>, 256, 0, nslots, cus));
       gext[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, false, kQuant>, 256, 0, nslots, cus));
     }
+    if (plan.bounces_run) *plan.bounces_run = 0;
     for (int b = 0; b < plan.max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
+      if (plan.bounces_run) *plan.bounces_run = b + 1;
       for (int t = 0; t < nt; ++t) {
         const WaveArgs& a = as[t];
         const hipStream_t st = sts[t];

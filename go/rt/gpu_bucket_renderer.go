@@ -59,11 +59,22 @@ func (g *GPUBucketRenderer) initGPU(camera *Camera, world Hittable) error {
 	if err != nil {
 		return err
 	}
-	if g.gpu, err = rtgpu.New(); err != nil { // every visible device
-		return err
+	// every visible device; if that context cannot be made (a device without
+	// peer access to device 0) or a device fails the upload (out of memory),
+	// device 0 alone before giving up on the GPU
+	if g.gpu, err = rtgpu.New(); err == nil {
+		if err = g.gpu.Upload(scene); err != nil {
+			g.gpu.Close()
+			g.gpu = nil
+		}
 	}
-	if err = g.gpu.Upload(scene); err != nil {
-		return err
+	if g.gpu == nil {
+		if g.gpu, err = rtgpu.New(0); err != nil {
+			return err
+		}
+		if err = g.gpu.Upload(scene); err != nil {
+			return err
+		}
 	}
 	g.cam = GPUCameraDesc(camera)
 	g.buckets = make([]rtgpu.Bucket, len(g.BucketRenderer.buckets))
@@ -142,32 +153,51 @@ func (g *GPUBucketRenderer) passErr() error {
 	return g.err
 }
 
-// gpuPass renders the current pass in one call over every device (each
-// render deals the buckets round-robin over the context's GPUs and
-// overwrites their sums, as renderBucketWithQuality writes every bucket
-// pixel each pass), quantised on the device with bucket_renderer.go:276-285's
-// formula (rt_render_rgba8: only the RGBA8 frame crosses PCIe), and copies it
-// into the framebuffer bucket by bucket under r.mu, as renderBucketWithQuality
-// does.
+// passChunk is the device work per rt_render_rgba8 call of a pass: long
+// enough that a call's fixed cost (its last kernels' tails, the RGBA8 copy)
+// stays a few per cent, short enough that the progress bar moves several
+// times a second.
+const passChunk = 150 * time.Millisecond
+
+// gpuPass renders the current pass over every device (each call deals its
+// buckets round-robin over the context's GPUs and overwrites their sums, as
+// renderBucketWithQuality writes every bucket pixel each pass), quantised on
+// the device with bucket_renderer.go:276-285's formula (rt_render_rgba8:
+// only the RGBA8 frame crosses PCIe).  It goes in calls of about passChunk
+// of work (the first 64 buckets, later ones sized from the previous call's
+// rate); after each call it copies that call's buckets into the framebuffer
+// under r.mu and advances completedCount by them, as renderBucketWithQuality
+// does bucket by bucket, so the window's progress bar moves during a pass.
 func (g *GPUBucketRenderer) gpuPass() {
 	r := g.BucketRenderer
 	spp, depth := passQuality(r.currentPass, r.camera)
 	w := r.camera.ImageWidth
 	seed := g.seed + uint32(r.currentPass)*0x9E3779B9 // one RNG stream per pass
-	_, err := g.gpu.RenderRGBA(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
-		Buckets: g.buckets}, g.rgba)
-	r.mu.Lock()
-	if err != nil {
-		g.err = err
-	} else {
-		for _, b := range g.buckets {
+	n := 64
+	for i := 0; i < len(g.buckets); {
+		chunk := g.buckets[i:min(i+n, len(g.buckets))]
+		t0 := time.Now()
+		_, err := g.gpu.RenderRGBA(&g.cam, rtgpu.RenderParams{SamplesPerPixel: spp, MaxDepth: depth, Seed: seed,
+			Buckets: chunk}, g.rgba)
+		el := time.Since(t0)
+		r.mu.Lock()
+		if err != nil {
+			g.err = err
+			r.mu.Unlock()
+			break
+		}
+		for _, b := range chunk {
 			for y := int(b.Y); y < int(b.Y+b.Height); y++ {
 				row := (y*w + int(b.X)) * 4
 				copy(r.framebuffer.Pix[row:row+int(b.Width)*4], g.rgba[row:row+int(b.Width)*4])
 			}
 		}
+		r.mu.Unlock()
+		r.completedCount.Add(int32(len(chunk)))
+		i += len(chunk)
+		if el > 0 {
+			n = min(max(int(float64(len(chunk))*float64(passChunk)/float64(el)), 16), len(g.buckets))
+		}
 	}
-	r.mu.Unlock()
-	r.completedCount.Add(int32(len(g.buckets)))
 	r.passComplete.Store(true)
 }

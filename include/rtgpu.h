@@ -392,6 +392,10 @@ int rt_tonemap_rgba8(rt_ctx* ctx, const float* accum_rgb, int32_t width, int32_t
  * rgba_out.  Pixels outside the buckets keep their previous RGBA8 value.
  * Only the 4 B/px framebuffer crosses PCIe (rt_render + rt_tonemap_rgba8
  * move 28 B/px).  A new image size starts from zero.  Blocks.
+ * The quantisation divides by the samples the sums hold: samples_per_pixel
+ * for an overwriting pass; with accumulate, sample_offset +
+ * samples_per_pixel (an accumulating pass continues the earlier passes'
+ * samples, so its sample_offset counts them).
  * stats->kernel_ms is the call's wall time.                               */
 int rt_render_rgba8(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                     uint8_t* rgba_out, rt_stats* stats);
@@ -408,9 +412,28 @@ int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32
 
 /* The same ids from the production pipeline: the hit records the render's
  * first-bounce closest-hit kernel (k_extend, persistent, with the context's
- * schedule options) writes for sample `sample` of every pixel.            */
+ * schedule options) writes for sample `sample` of every pixel
+ * (= rt_extend_hits at bounce 0).                                         */
 int rt_extend_first_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
                          int32_t* out_top, int32_t* out_prim, float* out_t);
+
+/* Path probes past the camera ray: world.Hit of every bounce (camera.go:449
+ * in rayColorInternal's recursion) and the NEE shadow rays (camera.go:582,
+ * :639), read back from the production pipeline.  Sample `sample` of every
+ * pixel is rendered to depth bounce + 1 (the rays of bounce k do not depend
+ * on the depth past it), so the records of bounce `bounce` are the last the
+ * pipeline wrote.
+ * rt_extend_hits: the closest hit of the path's bounce-`bounce` ray, ids as
+ * rt_primary_hits (-1 miss; -2 and t = -1: the path ended before this
+ * bounce), lifted volumes included; out_ray (may be NULL): the incoming ray,
+ * origin xyz and direction xyz (6 floats per pixel, 0 for ended paths).
+ * rt_shadow_visibility: per pixel, bit 0 / 1 = the area-light / HDRI shadow
+ * ray the bounce traced (a lifted volume that occludes a ray is resolved in
+ * shading and leaves its bit clear), bit 2 / 3 = that ray was unoccluded.  */
+int rt_extend_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t bounce,
+                   int32_t* out_top, int32_t* out_prim, float* out_t, float* out_ray);
+int rt_shadow_visibility(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sample, int32_t bounce,
+                         int32_t* out_nee);
 
 #ifdef __cplusplus
 }

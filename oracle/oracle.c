@@ -282,6 +282,26 @@ int oracle_primary_hits(const rt_scene_desc* scene, const rt_camera_desc* cam, u
   return rc;
 }
 
+int oracle_path_records(const rt_scene_desc* scene, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
+                        int32_t num_bounces, int fp32, int nthreads, int32_t* top, int32_t* prim, double* t,
+                        double* ray, int32_t* nee) {
+  if (!scene || !cam || !top || !prim || !t || !ray || !nee || num_bounces <= 0) return RT_ERR_INVALID;
+  const size_t n = (size_t)cam->image_width * (size_t)cam->image_height * (size_t)num_bounces;
+  for (size_t i = 0; i < n; ++i) {
+    top[i] = prim[i] = -2;
+    t[i] = -1.0;
+    nee[i] = 0;
+  }
+  memset(ray, 0, n * 6 * sizeof(double));
+  OScene os;
+  int rc = oscene_init(&os, scene);
+  if (rc) return rc;
+  rc = fp32 ? paths_f(&os, cam, seed, sample, num_bounces, nthreads, top, prim, t, ray, nee)
+            : paths_d(&os, cam, seed, sample, num_bounces, nthreads, top, prim, t, ray, nee);
+  oscene_free(&os);
+  return rc;
+}
+
 void oracle_tonemap(const float* accum, int64_t npix, int32_t spp, uint8_t* rgba) {   /* bucket_renderer.go:276-285 */
   double sc = 1.0 / (double)spp;
   for (int64_t i = 0; i < npix; ++i) {

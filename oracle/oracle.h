@@ -39,6 +39,16 @@ int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* cam, const r
 int oracle_primary_hits(const rt_scene_desc* scene, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
                         int fp32, int32_t* out_top, int32_t* out_prim, double* out_t);
 
+/* Every bounce b < num_bounces of sample `sample` of every pixel (element
+ * b * W*H + pixel), rayColorInternal to depth num_bounces: world.Hit ids
+ * (-1 miss, -2 path ended) and t (-1) of the bounce's ray, that ray (o, d:
+ * 6 per element) and its NEE shadow rays (bits 0/1 area/HDRI ray traced with
+ * a light term that counts, 2/3 unoccluded) — rt_extend_hits /
+ * rt_shadow_visibility's conventions. */
+int oracle_path_records(const rt_scene_desc* scene, const rt_camera_desc* cam, uint32_t seed, int32_t sample,
+                        int32_t num_bounces, int fp32, int nthreads, int32_t* top, int32_t* prim, double* t,
+                        double* ray, int32_t* nee);
+
 /* bucket_renderer.go:276-285 quantisation of a float sum (fp64 math). */
 void oracle_tonemap(const float* accum, int64_t npix, int32_t spp, uint8_t* rgba);
 

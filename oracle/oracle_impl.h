@@ -134,6 +134,15 @@ typedef struct {
   uint32_t bounce;
   uint32_t voldom;
   int* volcount;                 /* per vol_id Hit-call counter for this traversal */
+  /* path recorder (oracle_path_records; NULL r_top: off): per bounce b < r_nb,
+   * element b * r_npix + r_pix */
+  int32_t* r_top;
+  int32_t* r_prim;
+  double* r_t;
+  double* r_ray;                 /* 6 per element: incoming ray o, d */
+  int32_t* r_nee;                /* bits 0/1 area/HDRI shadow ray traced, 2/3 unoccluded */
+  int r_nb;
+  size_t r_npix, r_pix;
 } FN(TC);
 
 static inline REAL FN(rnd)(const FN(TC)* c, uint32_t dom, uint32_t idx) {
@@ -603,7 +612,10 @@ static V3R FN(sample_lights)(FN(TC)* c, const FN(Rec)* rec, V3R rdir, V3R att) {
       FN(Ray) sr;
       sr.o = rec->P; sr.d = ldir; sr.tm = 0;
       FN(Rec) srec;
-      if (!FN(world_hit)(c, O_DOM_VOL_SH_HDRI, sr, (REAL)0.001, (REAL)INFINITY, &srec)) {
+      const int occluded = FN(world_hit)(c, O_DOM_VOL_SH_HDRI, sr, (REAL)0.001, (REAL)INFINITY, &srec);
+      if (c->r_nee && (int)c->bounce < c->r_nb)                             /* path recorder */
+        c->r_nee[(size_t)c->bounce * c->r_npix + c->r_pix] |= 2 | (occluded ? 0 : 8);
+      if (!occluded) {
         REAL c2 = FN(dot)(rec->N, ldir);
         REAL pdfB = c2 < 0 ? 0 : c2 / PI_R;                                   /* Lambertian.PDF */
         REAL w = pdfH / (pdfH + pdfB);
@@ -628,7 +640,11 @@ static V3R FN(sample_lights)(FN(TC)* c, const FN(Rec)* rec, V3R rdir, V3R att) {
         FN(Ray) sr;
         sr.o = rec->P; sr.d = ldir; sr.tm = 0;
         FN(Rec) srec;
-        if (!FN(world_hit)(c, O_DOM_VOL_SH_AREA, sr, (REAL)0.001, dist - (REAL)0.001, &srec)) {
+        const int occluded = FN(world_hit)(c, O_DOM_VOL_SH_AREA, sr, (REAL)0.001, dist - (REAL)0.001, &srec);
+        if (c->r_nee && (int)c->bounce < c->r_nb &&                         /* path recorder: a ray whose */
+            !(FABS(FN(dot)(FN(mk)(p[12], p[13], p[14]), FN(neg)(ldir))) < (REAL)0.001))   /* light term counts */
+          c->r_nee[(size_t)c->bounce * c->r_npix + c->r_pix] |= 1 | (occluded ? 0 : 4);
+        if (!occluded) {
           const rt_material* lm = &d->materials[lh->material];
           V3R em = lm->kind == RT_DIFFUSE_LIGHT ? FN(tex_value)(S, lm->texture, 0, 0, lp) : FN(mk)(0, 0, 0);
           REAL area = FN(len)(FN(cross)(lu, lv));
@@ -655,7 +671,16 @@ static V3R FN(ray_color)(FN(TC)* c, FN(Ray) r, int depth, uint32_t bounce, int a
   if (depth <= 0) return FN(mk)(0, 0, 0);
   c->bounce = bounce;
   FN(Rec) rec;
-  if (!FN(world_hit)(c, O_DOM_VOL, r, (REAL)0.001, (REAL)INFINITY, &rec)) {
+  const int hit = FN(world_hit)(c, O_DOM_VOL, r, (REAL)0.001, (REAL)INFINITY, &rec);
+  if (c->r_top && (int)bounce < c->r_nb) {                                   /* path recorder */
+    const size_t e = (size_t)bounce * c->r_npix + c->r_pix;
+    c->r_top[e] = hit ? rec.top : -1;
+    c->r_prim[e] = hit ? rec.prim : -1;
+    c->r_t[e] = hit ? (double)rec.t : -1.0;
+    const double ray[6] = {(double)r.o.x, (double)r.o.y, (double)r.o.z, (double)r.d.x, (double)r.d.y, (double)r.d.z};
+    memcpy(c->r_ray + e * 6, ray, sizeof ray);
+  }
+  if (!hit) {
     if (os->env_valid) {
       if (S->cam_phantom && depth == S->cam_max_depth) return FN(mk)(0, 0, 0);
       return FN(env_sample)(S, r.d);
@@ -877,6 +902,62 @@ static int FN(primary)(const OScene* os, const rt_camera_desc* cam, uint32_t see
       tout[pix] = h ? (double)rec.t : -1.0;
     }
   free(vc);
+  FN(unprep)(&S);
+  return 0;
+}
+
+/* Every bounce of one sample per pixel (rayColorInternal camera.go:443-518 to
+ * depth nb): world.Hit ids, t and the incoming ray per bounce, the NEE
+ * shadow rays traced and their visibility (sampleHDRILight :582,
+ * sampleAreaLight :639).  Outputs are filled by the caller (ended paths keep
+ * the fill).  Pixels are split over nthreads. */
+typedef struct {
+  const FN(OS)* S;
+  uint32_t seed;
+  int sample, nb, t0, nth;
+  int32_t *top, *prim, *nee;
+  double *t, *ray;
+} FN(PJob);
+
+static void* FN(path_worker)(void* arg) {
+  FN(PJob)* J = (FN(PJob)*)arg;
+  const FN(OS)* S = J->S;
+  int* vc = (int*)calloc((size_t)(S->os->nvol > 0 ? S->os->nvol : 1), sizeof(int));
+  FN(TC) c;
+  memset(&c, 0, sizeof(c));
+  c.S = S;
+  c.volcount = vc;
+  c.r_top = J->top; c.r_prim = J->prim; c.r_t = J->t; c.r_ray = J->ray; c.r_nee = J->nee;
+  c.r_nb = J->nb;
+  const int W = S->cam_w, H = S->cam_h;
+  c.r_npix = (size_t)W * (size_t)H;
+  for (size_t pix = (size_t)J->t0; pix < c.r_npix; pix += (size_t)J->nth) {
+    c.r_pix = pix;
+    c.key = o_path_key(J->seed, (uint32_t)pix, (uint32_t)J->sample);
+    FN(Ray) r = FN(get_ray)(&c, (int)(pix % (size_t)W), (int)(pix / (size_t)W));
+    (void)FN(ray_color)(&c, r, J->nb, 0, 1);
+  }
+  (void)H;
+  free(vc);
+  return NULL;
+}
+
+static int FN(paths)(const OScene* os, const rt_camera_desc* cam, uint32_t seed, int sample, int nb, int nthreads,
+                     int32_t* top, int32_t* prim, double* t, double* ray, int32_t* nee) {
+  FN(OS) S;
+  int rc = FN(prep)(&S, os, cam);
+  if (rc) return rc;
+  if (nthreads < 1) nthreads = 1;
+  FN(PJob)* J = (FN(PJob)*)malloc(sizeof(FN(PJob)) * (size_t)nthreads);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; ++i) {
+    J[i].S = &S; J[i].seed = seed; J[i].sample = sample; J[i].nb = nb; J[i].t0 = i; J[i].nth = nthreads;
+    J[i].top = top; J[i].prim = prim; J[i].nee = nee; J[i].t = t; J[i].ray = ray;
+    pthread_create(&th[i], NULL, FN(path_worker), &J[i]);
+  }
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  free(J);
   FN(unprep)(&S);
   return 0;
 }

@@ -31,6 +31,9 @@ def lib():
         L.oracle_render.argtypes = [P, P, P, C.c_int, C.c_int, C.POINTER(C.c_double)]
         L.oracle_primary_hits.argtypes = [P, P, C.c_uint32, C.c_int32, C.c_int, C.POINTER(C.c_int32),
                                           C.POINTER(C.c_int32), C.POINTER(C.c_double)]
+        L.oracle_path_records.argtypes = [P, P, C.c_uint32, C.c_int32, C.c_int32, C.c_int, C.c_int,
+                                          C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                                          C.POINTER(C.c_double), C.POINTER(C.c_int32)]
         L.oracle_tonemap.argtypes = [C.POINTER(C.c_float), C.c_int64, C.c_int32, C.POINTER(C.c_uint8)]
         L.oracle_tonemap.restype = None
         L.oracle_rng_uniform.argtypes = [C.c_uint32] * 4
@@ -75,6 +78,26 @@ def primary_hits(scene_desc, camera, seed: int, sample: int = 0, fp32: bool = Tr
     if rc != 0:
         raise RuntimeError(f"oracle_primary_hits failed: {rc}")
     return top, prim, t
+
+
+def path_records(scene_desc, camera, seed: int, sample: int, num_bounces: int, fp32: bool = True, threads: int = 0):
+    """Per bounce b < num_bounces (arrays of shape (num_bounces, W*H)): top,
+    prim (-1 miss, -2 path ended), t, the incoming ray (..., 6) and the NEE
+    bits (oracle.h oracle_path_records)."""
+    n = camera.image_width * camera.image_height
+    top = np.zeros((num_bounces, n), np.int32)
+    prim = np.zeros((num_bounces, n), np.int32)
+    t = np.zeros((num_bounces, n), np.float64)
+    ray = np.zeros((num_bounces, n, 6), np.float64)
+    nee = np.zeros((num_bounces, n), np.int32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    rc = lib().oracle_path_records(_ptr(scene_desc), _ptr(camera), seed, sample, num_bounces, 1 if fp32 else 0, threads,
+                                   top.ctypes.data_as(C.POINTER(C.c_int32)), prim.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   t.ctypes.data_as(C.POINTER(C.c_double)), ray.ctypes.data_as(C.POINTER(C.c_double)),
+                                   nee.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc != 0:
+        raise RuntimeError(f"oracle_path_records failed: {rc}")
+    return top, prim, t, ray, nee
 
 
 def tonemap(accum_f32: np.ndarray, spp: int) -> np.ndarray:

@@ -107,6 +107,25 @@ class Builder:
         bb = self._pad([b[0] + off[0], b[1] + off[0], b[2] + off[1], b[3] + off[1], b[4] + off[2], b[5] + off[2]])
         return self._add(self.g.RT_TRANSLATE, -1, child, 0, bb, list(off))
 
+    def rotate_y(self, child, sin_t, cos_t):
+        """RotateY (transform.go:113-157): bbox = the child's corners rotated."""
+        b = self.h[child].bbox
+        pts = np.array([[x, y, z] for x in b[0:2] for y in b[2:4] for z in b[4:6]], float)
+        nx = cos_t * pts[:, 0] + sin_t * pts[:, 2]
+        nz = -sin_t * pts[:, 0] + cos_t * pts[:, 2]
+        bb = [nx.min(), nx.max(), pts[:, 1].min(), pts[:, 1].max(), nz.min(), nz.max()]
+        return self._add(self.g.RT_ROTATE_Y, -1, child, 0, self._pad(bb), [sin_t, cos_t])
+
+    def scale(self, child, f):
+        """Scale (transform.go:360-403): bbox corners times the factor."""
+        b = self.h[child].bbox
+        lo = [b[0] * f[0], b[2] * f[1], b[4] * f[2]]
+        hi = [b[1] * f[0], b[3] * f[1], b[5] * f[2]]
+        bb = []
+        for a in range(3):
+            bb += [min(lo[a], hi[a]), max(lo[a], hi[a])]
+        return self._add(self.g.RT_SCALE, -1, child, 0, self._pad(bb), list(f) + [1.0 / x for x in f])
+
     def volume(self, boundary, density, mat):
         return self._add(self.g.RT_VOLUME, mat, boundary, 0, list(self.h[boundary].bbox), [-1.0 / density])
 

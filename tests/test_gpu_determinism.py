@@ -98,6 +98,30 @@ def test_other_configs_schedule_independent(g, name, kw):
         c.close()
 
 
+@pytest.mark.parametrize("streams", [3, 4])
+def test_many_streams_fresh_context(g, streams):
+    """Three / four twins on a fresh context whose batch buffers are sized
+    exactly for this render (no larger earlier batch, one batch per frame):
+    every twin's queue counters and NEE job words lie inside the allocation
+    (api.cpp render_wave checks the slices before launching) and the frame
+    equals the one-stream frame bit for bit."""
+    s = g.Scene("cornell", width=96)
+    cam = s.camera
+    npix = cam.image_width * cam.image_height
+    spp = 8
+    p = g.make_params(spp, cam.max_depth, seed=SEED)
+    frames = []
+    for st in (streams, 1):
+        c = g.Context(0)
+        try:
+            c.upload(s.desc)
+            c.set_schedule(npix * spp, 0, 0, st)
+            frames.append(c.render(cam, p)[0])
+        finally:
+            c.close()
+    assert np.array_equal(frames[0], frames[1])
+
+
 def test_schedule_option_validation(g, ctx):
     with pytest.raises(g.RTError):
         ctx.set_option(g.RT_OPT_REFILL, 65)

@@ -91,7 +91,11 @@ def test_radiance_parity_fp32(g, O, ctx, name, kw):
     gpu, _ = ctx.render(cam, p)
     ref = O.render(s.desc, cam, p, fp32=True)
     assert np.isfinite(gpu).all()
-    mse = float(np.mean((gpu.astype(np.float64) / spp - ref / spp) ** 2))
+    a, b = gpu.astype(np.float64) / spp, ref / spp
+    mse = float(np.mean((a - b) ** 2))
+    px_err = np.max(np.abs(a - b), axis=2)
+    differ = float(np.mean(px_err > 1e-5 * np.maximum(1.0, np.max(np.abs(b), axis=2))))
+    print(f"fp32 parity {name}: mse {mse:.3e} max |d| {px_err.max():.3e} pixels off by >1e-5 rel {differ:.2e}")
     assert mse < 1e-4, f"{name}: mse {mse:.3e}"
     assert gpu.mean() > 0
 

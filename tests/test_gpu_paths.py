@@ -1,0 +1,86 @@
+"""Integer hit work past the camera ray (north_star: "integer hit-index work
+bit-exact").
+
+rt_extend_hits reads back the hit records the production closest-hit kernel
+(k_extend) wrote at bounce k, with the incoming ray it traced;
+rt_shadow_visibility reads the NEE shadow jobs of bounce k and what the
+any-hit kernel (k_shadow) found.  The fp32 oracle records the same per bounce
+while it walks the caller's reference BVH recursively (rayColorInternal
+camera.go:443-518: world.Hit at :449, sampleHDRILight's shadow ray :582,
+sampleAreaLight's :639).
+
+For every path whose incoming ray is bit-identical on both sides, the hit ids
+and t must be equal, and so must the NEE rays traced and their visibility
+(a lifted volume occluding a shadow ray is resolved in shading: the GPU then
+has no such ray, the oracle an occluded one).  Paths whose rays differ
+("diverged": an earlier bounce rounded differently) are counted and reported
+and bounded, never compared.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 29
+BOUNCES = 5
+# (scene, constructor kwargs, samples probed, max share of diverged paths)
+CASES = [
+    ("cornell-lucy", dict(width=320, aspect=16.0 / 9.0), (0, 5), 2e-3),   # C4, full 280K mesh
+    ("cornell", dict(width=128), (0, 5), 2e-3),                           # C3, fog + area light
+    ("random", dict(width=192), (0, 5), 2e-3),                            # C2, spheres, metal, glass
+    ("cornell-smoke", dict(width=96), (0,), 2e-3),                        # two lifted volumes
+    ("cornell-rotations", dict(width=96), (0,), 2e-3),                    # RotateX/Z, Scale chains
+    ("hdri-nee", dict(width=96), (0,), 2e-2),                             # HDRI importance sampling + area light
+]
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def compare_paths(g, O, name, kw, samples):
+    """Per bounce and sample: (alive paths, compared, diverged, id/t mismatches,
+    NEE mismatches).  Raises nothing; the caller asserts."""
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    c = g.Context(0)
+    rows = []
+    try:
+        c.upload(s.desc)
+        lifted = c.info().volumes > 0
+        for sample in samples:
+            ot, op, ott, oray, onee = O.path_records(s.desc, cam, SEED, sample, BOUNCES, fp32=True, threads=16)
+            for b in range(BOUNCES):
+                gt, gp, gtt, gray = c.extend_hits(cam, SEED, sample, b)
+                gnee = c.shadow_visibility(cam, SEED, sample, b)
+                alive_g, alive_o = gt != -2, ot[b] != -2
+                same_ray = alive_g & alive_o & np.all(_bits(gray) == _bits(oray[b]), axis=1)
+                div = (alive_g | alive_o) & ~same_ray
+                hit_bad = same_ray & ((gt != ot[b]) | (gp != op[b]) | (_bits(gtt) != _bits(ott[b])))
+                ok = same_ray & ~hit_bad
+                gf, gv = gnee & 3, (gnee >> 2) & 3
+                of, ov = onee[b] & 3, (onee[b] >> 2) & 3
+                nee_bad = ok & (((gv & ~gf) != 0) | (gv != ov) | ((gf & ~of) != 0))
+                if not lifted:
+                    nee_bad |= ok & (gf != of)
+                rows.append(dict(sample=sample, bounce=b, alive=int(np.sum(alive_g | alive_o)),
+                                 compared=int(np.sum(same_ray)), diverged=int(np.sum(div)),
+                                 hit_mismatch=int(np.sum(hit_bad)), nee_mismatch=int(np.sum(nee_bad)),
+                                 shadow_rays=int(np.sum(((gf & 1) != 0).astype(int) + ((gf & 2) != 0))),
+                                 first_bad=np.flatnonzero(hit_bad | nee_bad)[:4].tolist()))
+    finally:
+        c.close()
+    return rows
+
+
+@pytest.mark.parametrize("name,kw,samples,max_div", CASES, ids=[c[0] for c in CASES])
+def test_bounce_hits_and_shadow_rays_bit_exact(g, O, name, kw, samples, max_div):
+    rows = compare_paths(g, O, name, kw, samples)
+    for r in rows:
+        print(f"{name} sample {r['sample']} bounce {r['bounce']}: alive {r['alive']} compared {r['compared']} "
+              f"diverged {r['diverged']} shadow rays {r['shadow_rays']} hit mismatches {r['hit_mismatch']} "
+              f"NEE mismatches {r['nee_mismatch']}")
+    assert sum(r["compared"] for r in rows if r["bounce"] > 0) > 0
+    for r in rows:
+        assert r["hit_mismatch"] == 0 and r["nee_mismatch"] == 0, f"{name}: {r}"
+        assert r["diverged"] <= max_div * max(r["alive"], 1), f"{name}: too many diverged paths {r}"

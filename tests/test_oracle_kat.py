@@ -223,3 +223,68 @@ def test_fp32_mirror_close_to_fp64(g, O):
     b = O.render(s.desc, cam, p, fp32=True) / 16
     assert abs(a.mean() - b.mean()) < 0.02 * a.mean()
     assert float(np.mean((a - b) ** 2)) < 5e-3
+
+
+# ---- NEE, instance transforms, volumes (tests/kat_cases.py) ---------------
+from tests import kat_cases as K  # noqa: E402
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_area_light_nee_closed_form(g, O, fp32):
+    """sampleAreaLight (camera.go:610-678): cosines, pdfL, balance weight,
+    x number of lights, per-component clamp at 20 (red clamps)."""
+    b, d, cam = K.area_light_scene(g)
+    got = O.render(d, cam, g.make_params(4, 1, seed=K.SEED), fp32=fp32)[0]
+    want = K.area_light_expected(spp=4)
+    assert (want[:, 0] == 80.0).any() and (want[:, 0] < 80.0).any() and (want[:, 1] < 20).all()   # red clamps
+    np.testing.assert_allclose(got, want, rtol=2e-5 if fp32 else 1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_instance_chain_point_and_normal(g, O, fp32):
+    """Translate(RotateY(Scale(quad))): t = 1 in every space, the bounce-1 ray
+    starts at the world hit point and leaves along N + RandomUnitVector with
+    N renormalised by Scale and rotated back (transform.go:113-191, 360-444)."""
+    b, d, cam, top, q = K.instance_scene(g)
+    t_top, t_prim, t_t, ray, _ = O.path_records(d, cam, K.SEED, 0, 2, fp32=fp32, threads=2)
+    assert (t_top[0] == top).all() and (t_prim[0] == q).all()
+    tol = 2e-6 if fp32 else 1e-12
+    np.testing.assert_allclose(t_t[0], 1.0, rtol=tol)
+    P = K.instance_world_point()
+    N = K.instance_expected_normal()
+    assert abs(np.linalg.norm(N) - 1) < 1e-12 and N[1] < 0
+    for pix in range(cam.image_width):
+        assert t_top[1, pix] != -2
+        np.testing.assert_allclose(ray[1, pix, :3], P, rtol=tol * 4, atol=tol * 4)
+        n_got = ray[1, pix, 3:] - K.random_unit_vector(K.SEED, pix, 0, 0)
+        np.testing.assert_allclose(n_got, N, rtol=0, atol=tol * 8)
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_volume_hit_fixed_draw(g, O, fp32):
+    """Volume.Hit (volume.go:34-79): t1 = 2, t2 = 4, the free flight
+    -ln(U)/rho from the pixel's draw; a longer flight passes to the wall."""
+    b, d, cam, vol, back = K.volume_scene(g)
+    top, prim, t = O.primary_hits(d, cam, K.SEED, 0, fp32=fp32)
+    ids, ts = K.volume_expected()
+    want = np.array([vol if i == "vol" else back for i in ids])
+    assert np.array_equal(prim, want)
+    assert 0.2 < (want == vol).mean() < 0.8
+    np.testing.assert_allclose(t, ts, rtol=2e-6 if fp32 else 1e-12)
+
+
+@pytest.mark.parametrize("name,kw", [("cornell", dict(width=48)), ("hdri-nee", dict(width=48)),
+                                     ("cornell-smoke", dict(width=48))])
+def test_path_records_consistent(g, O, name, kw):
+    """The oracle's per-bounce recorder: bounce 0 is primary_hits, a path that
+    ended stays ended, a visible shadow ray is a traced one."""
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    top, prim, t, ray, nee = O.path_records(s.desc, cam, 5, 1, 4, fp32=True, threads=4)
+    pt, pp, ptt = O.primary_hits(s.desc, cam, 5, 1, fp32=True)
+    assert np.array_equal(top[0], pt) and np.array_equal(prim[0], pp) and np.array_equal(t[0], ptt)
+    for k in range(1, 4):
+        assert not ((top[k - 1] == -2) & (top[k] != -2)).any()
+        assert not ((top[k - 1] == -1) & (top[k] != -2)).any()      # a miss ends the path
+    assert ((nee >> 2) & ~nee & 3 == 0).all()
+    assert ((nee >> 2) & 3).any()
