@@ -825,7 +825,7 @@ static int device_builds(rt_ctx* ctx) {
     HIPCHK(hipMemcpyAsync(const_cast<DBvh*>(d.blas) + j.blas, &h.blas[size_t(j.blas)], sizeof(DBvh), hipMemcpyHostToDevice,
                           ctx->stream));
   }
-  h.stack_needed = h.tlas_need4 + h.max_leaf_inst + 1 + need + 2;
+  h.stack_needed = (h.tlas_need4 + h.max_leaf_inst + 1 + need + 2) * (h.dfs_order ? 2 : 1);
   if (h.stack_needed > kStackMax)
     return set_err(ctx, RT_ERR_UNSUPPORTED, "device-built BVH too deep for the traversal stack");
   d.stack_needed = h.stack_needed;
@@ -908,6 +908,7 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed;
   d.quant_nodes = h.quant_nodes;
+  d.dfs_order = h.dfs_order;
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());

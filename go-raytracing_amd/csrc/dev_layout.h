@@ -356,6 +356,7 @@ struct DScene {
   int32_t shade_kind;     // SHADE_LEAN / MAT / FULL / VOL: the k_shade variant
   int32_t needs_uv;       // an ImageTexture exists: hit records carry U/V
   int32_t quant_nodes;    // traverse the quantised DNodeQ nodes (RT_NODES_QUANT8), else DNode4
+  int32_t dfs_order;      // closest hit in the reference's DFS order with exact box culls (RotateX/Z scenes; trav_step)
   // array lengths (bounds checks of the RTG_GUARD diagnostic build)
   uint32_t n_nodes, n_leaves, n_refs, n_spheres, n_quads, n_tris, n_instances, n_blas, n_volumes, n_circles;
 };

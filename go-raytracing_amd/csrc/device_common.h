@@ -800,11 +800,38 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
 //   kQuant = true: the node records are DNodeQ (RT_NODES_QUANT8), else DNode4.
 template <bool kAny, bool kCount, bool kVol, bool kQuant = false>
 __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
-  auto pop = [&]() -> uint32_t { if (T.sp == 0) return ITEM_NONE; --T.sp; return S.pop(T.sp); };
+  // Reference-order mode (DScene.dfs_order; only in the rare-primitive kVol
+  // variant, closest hit): scenes holding a RotateX / RotateZ wrapper, whose
+  // bbox does not contain what its Hit sees (transform.go:201-351), so which
+  // rays reach it depends on the closest distance at the moment the
+  // reference's left-first DFS (bvh.go:219-239) tests each enclosing node
+  // box.  Children are then visited in DFS order, every box is culled
+  // against the exact closest distance, and a pushed child keeps its entry
+  // distance beside it on the stack and is culled again when popped — the
+  // moment the reference would test its box (a BVH4 node skips the BVH2
+  // nodes collapsed into it, whose boxes contain their children's and never
+  // cull a child that passes).  Each stack entry is then two words.
+  const bool exact = kVol && !kAny && sc.dfs_order != 0;
+  auto pop = [&]() -> uint32_t {
+    for (;;) {
+      if (T.sp == 0) return ITEM_NONE;
+      --T.sp;
+      const uint32_t v = S.pop(T.sp);
+      if (!exact) return v;
+      --T.sp;
+      const float te = __uint_as_float(S.pop(T.sp));
+      if (te < best_t(T)) return v;   // BVHNode.Hit's box test against the closest hit so far
+    }
+  };
   // The host bounds the stack need (flatten: stack_needed <= kStackMax), so an
   // overflow is an internal error: flagged for the host, the entry dropped,
-  // and no early exit in the push sequence.
-  auto push = [&](uint32_t v) {
+  // and no early exit in the push sequence.  `te`: the entry's box entry
+  // distance (reference-order mode; -inf = no box to test again).
+  auto push = [&](uint32_t v, float te = -__builtin_inff()) {
+    if (exact) {
+      S.push(T.sp, __float_as_uint(te), err);
+      ++T.sp;
+    }
     if (kCount && T.sp >= S.cap) cnt.spill++;
     S.push(T.sp, v, err);
     ++T.sp;
@@ -823,7 +850,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const bool st_lead = rtg_lead();
     const uint32_t st0 = rtg_stamp();
 #endif
-    const float hi = kAny ? T.tmax : T.bt;
+    const float hi = kAny ? T.tmax : exact ? best_t(T) : T.bt;
     const float inf = __builtin_inff();
     const uint32_t nidx = GIX(T.item & ITEM_MASK, sc.n_nodes, 9);
     float t0, t1, t2, t3;
@@ -911,11 +938,19 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
       const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
     };
-    cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2);
+    if (!exact) { cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2); }
 #ifdef RTG_STAMP
     const uint32_t st2 = rtg_stamp();
 #endif
-    if (!(t0 < inf)) {
+    if (exact) {
+      // reference order: the hit children pushed right to left with their
+      // entry distances, the leftmost popped (and so visited) first
+      if (t3 < inf) push(i3, t3);
+      if (t2 < inf) push(i2, t2);
+      if (t1 < inf) push(i1, t1);
+      if (t0 < inf) push(i0, t0);
+      T.item = pop();
+    } else if (!(t0 < inf)) {
       T.item = pop();
     } else {
       // (a branch-free three-slot LDS write when no spill is possible measured
@@ -1075,7 +1110,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       // several objects was culled there), then the wrapper chain (the ray
       // into object space, transform.go) and the BLAS root box.
       const bool winst = tag == ITEM_WINST;
-      const float hi = kAny ? T.tmax : T.bt;
+      const float hi = kAny ? T.tmax : exact ? best_t(T) : T.bt;
       float tn = 0.0f;
       bool go = true;
       if (winst) {

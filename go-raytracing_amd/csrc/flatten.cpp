@@ -1322,6 +1322,11 @@ struct Flattener {
     // scenes keep the fp32 DNode4 boxes whatever node format was asked for
     S.quant_nodes = opt.quant_nodes && tlas_sah_ok() ? 1 : 0;
     S.stack_needed = S.tlas_need4 + max_leaf_inst + 1 + S.blas_need4 + 2;
+    // the same scenes traverse in the reference's DFS order with exact box
+    // culls (trav_step's reference-order mode), which keeps each stack
+    // entry's box entry distance beside it: twice the words
+    S.dfs_order = tlas_sah_ok() ? 0 : 1;
+    if (S.dfs_order) S.stack_needed *= 2;
     if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
     if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27) || S.nodes4.size() >= (1u << 27))
       fail(RT_ERR_UNSUPPORTED, "scene too large for 28-bit indices");

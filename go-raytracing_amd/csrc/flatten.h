@@ -53,6 +53,7 @@ struct HostScene {
   int tlas_need4 = 0, blas_need4 = 0;   // BVH4 stack entries along the worst root-to-leaf path
   int max_leaf_inst = 0;                 // most instances in one world leaf (stack bound)
   int quant_nodes = 0;                   // the traversal reads DNodeQ (RT_NODES_QUANT8, no RotateX/Z)
+  int dfs_order = 0;                     // RotateX/Z scenes: reference-order closest hit (trav_step); two stack words per entry
   // Mesh BLASes left to the device builder (RT_BLAS_DEVICE): their triangles
   // are in the arrays in reference DFS order; the BLAS header's root item is
   // a placeholder until build_mesh_blas (build.hip) fills it in.

@@ -1024,7 +1024,8 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     if ((e = hipMemsetAsync(as[t].acc, 0, size_t(as[t].npix) * 3 * sizeof(double), sts[t])) != hipSuccess) return e;
   if (plan.max_depth > 0) {
     // the kVol variants also carry the rare primitives (circles)
-    const bool vol = sc.has_volumes != 0 || sc.n_circles > 0;
+    // (and the reference-order closest hit of RotateX/Z scenes, DScene.dfs_order)
+    const bool vol = sc.has_volumes != 0 || sc.n_circles > 0 || sc.dfs_order != 0;
 #define RUN3(S, C, V, E, Q)                                                          \
   do {                                                                               \
     if (shade == SHADE_FULL) e = run_batches<S, C, V, E, SHADE_FULL, Q>(sc, cam, as, sts, plan);        \

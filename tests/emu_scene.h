@@ -89,6 +89,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.num_materials = int(h.materials.size()); d.num_textures = int(h.textures.size());
   d.stack_needed = h.stack_needed;
   d.quant_nodes = h.quant_nodes;
+  d.dfs_order = h.dfs_order;
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());

@@ -11,7 +11,7 @@ traversal is built so that none of that changes a hit (DESIGN.md §3
     identical under those schedules and equal, id for id and t for t, to the
     CPU oracle's fp32 mode (which walks the caller's reference BVH in Go's
     DFS order, bvh.go:219-239);
-  * the radiance matches the fp32 oracle within the parity bar (mse < 1e-4).
+  * the radiance matches the fp32 oracle within the fp32 bar (test_gpu_parity.fp32_bar).
 
 CornellBoxLucy with the full 280K-triangle mesh at 320x180, 16 spp.
 """
@@ -70,9 +70,8 @@ def test_c4_full_mesh_schedule_independent(g, O, lucy):
         tp, pp, _ = c.primary_hits(cam, SEED, 0)
         assert np.array_equal(tp, hits[0][0][0]) and np.array_equal(pp, hits[0][0][1])
         ref = O.render(lucy.desc, cam, p, fp32=True, threads=16)
-        mse = float(np.mean((frames[0].astype(np.float64) / SPP - ref / SPP) ** 2))
-        print(f"C4 320x180 {SPP}spp full mesh: 3 schedules bit-identical, mse vs fp32 oracle {mse:.3e}")
-        assert mse < 1e-4
+        from tests.test_gpu_parity import fp32_bar
+        mse, _ = fp32_bar("C4 320x180 16spp full mesh, 5 schedules bit-identical", frames[0], ref, SPP)
     finally:
         c.close()
 

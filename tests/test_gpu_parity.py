@@ -3,9 +3,18 @@
 Tolerances (stated, BASELINE.json north_star):
   * first-bounce closest-hit ids (top-level object, primitive) and hit t:
     bit-exact vs the oracle's fp32 mirror mode, every scene (fog included: the
-    free-flight log is libm-free on both sides, tests/test_detlog.py);
-  * radiance vs the fp32 mirror: image mean over pixels of the squared RGB
-    error of the per-pixel average radiance < 1e-4 (same counter RNG keys);
+    free-flight log is libm-free on both sides, tests/test_detlog.py); every
+    later bounce and every NEE shadow ray: tests/test_gpu_paths.py;
+  * radiance vs the fp32 mirror (same counter RNG keys, so every path is the
+    same path, tests/test_gpu_paths.py): image mean over pixels of the squared
+    RGB error of the per-pixel average radiance <= FP32_MSE = 1e-10, and at
+    most FP32_OFF = 1e-3 of the pixels (HDRI scenes: FP32_OFF_HDRI = 1e-2)
+    off by more than 1e-5 relative.  What remains is the order of the adds
+    (the GPU adds beta * emission bounce by bounce, the recursion returns
+    Le + att * L) and, with an HDRI, the last-ulp differences of ocml's and
+    glibc's atan2f / asinf / sinf / cosf in the environment lookups.
+    Measured (round 4): mse <= 3.9e-16, max |d| <= 4.7e-7, no pixel off;
+    HDRI scenes mse 6.9e-12, max |d| 1.0e-4, 0.27-0.52 % of the pixels off;
   * radiance vs the oracle's float64 mode (the Go arithmetic, camera.go:443-518
     in float64) on the BASELINE configs: the same image-mean squared error
     <= 1e-4 at the spp stated per config in FP64_CASES, and the image-mean
@@ -16,6 +25,21 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+FP32_MSE = 1e-10
+FP32_OFF, FP32_OFF_HDRI = 1e-3, 1e-2
+
+
+def fp32_bar(name, gpu_sum, ref_sum, spp):
+    """(mse, share of pixels off by > 1e-5 relative); asserts the fp32 bar."""
+    a, b = gpu_sum.astype(np.float64) / spp, ref_sum / spp
+    mse = float(np.mean((a - b) ** 2))
+    px_err = np.max(np.abs(a - b), axis=2)
+    off = float(np.mean(px_err > 1e-5 * np.maximum(1.0, np.max(np.abs(b), axis=2))))
+    print(f"fp32 parity {name}: mse {mse:.3e} max |d| {px_err.max():.3e} pixels off by >1e-5 rel {off:.2e}")
+    assert mse <= FP32_MSE, f"{name}: mse {mse:.3e}"
+    assert off <= (FP32_OFF_HDRI if name.startswith("hdri") else FP32_OFF), f"{name}: {off:.3e} of the pixels off"
+    return mse, off
 
 LUCY = dict(lucy_rings=60, lucy_cols=80)
 SCENES = [
@@ -91,12 +115,7 @@ def test_radiance_parity_fp32(g, O, ctx, name, kw):
     gpu, _ = ctx.render(cam, p)
     ref = O.render(s.desc, cam, p, fp32=True)
     assert np.isfinite(gpu).all()
-    a, b = gpu.astype(np.float64) / spp, ref / spp
-    mse = float(np.mean((a - b) ** 2))
-    px_err = np.max(np.abs(a - b), axis=2)
-    differ = float(np.mean(px_err > 1e-5 * np.maximum(1.0, np.max(np.abs(b), axis=2))))
-    print(f"fp32 parity {name}: mse {mse:.3e} max |d| {px_err.max():.3e} pixels off by >1e-5 rel {differ:.2e}")
-    assert mse < 1e-4, f"{name}: mse {mse:.3e}"
+    fp32_bar(name, gpu, ref, spp)
     assert gpu.mean() > 0
 
 
@@ -120,8 +139,8 @@ def test_quant8_nodes_parity(g, O, name, kw):
         p = g.make_params(spp, cam.max_depth, seed=77)
         gpu, _ = c.render(cam, p)
         ref = O.render(s.desc, cam, p, fp32=True)
-        mse = float(np.mean((gpu.astype(np.float64) / spp - ref / spp) ** 2))
-        assert np.isfinite(gpu).all() and mse < 1e-4, f"{name}: mse {mse:.3e}"
+        assert np.isfinite(gpu).all()
+        fp32_bar(name, gpu, ref, spp)
     finally:
         c.close()
 
@@ -243,8 +262,7 @@ def test_bucket_renderer_three_passes(g, O, tmp_path, name):
         acc, fb = r.accum(), r.framebuffer()
         pseed = (seed + k * 0x9E3779B9) & 0xFFFFFFFF
         ref = O.render(s.desc, cam, g.make_params(spp, depth, seed=pseed, buckets=buckets), fp32=True)
-        mse = float(np.mean((acc.astype(np.float64) / spp - ref / spp) ** 2))
-        assert mse < 1e-4, f"pass {k}: mse {mse:.3e}"
+        mse, _ = fp32_bar(f"{name} pass {k}", acc, ref, spp)
         assert np.array_equal(fb, O.tonemap(acc, spp)), f"pass {k}: framebuffer is not the quantised accumulation"
         same = float(np.mean(fb == O.tonemap(ref.astype(np.float32), spp)))
         print(f"{name} pass {k} ({spp} spp, depth {depth}): mse {mse:.2e}, RGBA8 bytes equal to the oracle's {same:.5f}")

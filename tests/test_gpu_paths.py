@@ -63,11 +63,14 @@ def compare_paths(g, O, name, kw, samples):
                 nee_bad = ok & (((gv & ~gf) != 0) | (gv != ov) | ((gf & ~of) != 0))
                 if not lifted:
                     nee_bad |= ok & (gf != of)
+                bad = np.flatnonzero(hit_bad | nee_bad)[:4]
                 rows.append(dict(sample=sample, bounce=b, alive=int(np.sum(alive_g | alive_o)),
                                  compared=int(np.sum(same_ray)), diverged=int(np.sum(div)),
                                  hit_mismatch=int(np.sum(hit_bad)), nee_mismatch=int(np.sum(nee_bad)),
                                  shadow_rays=int(np.sum(((gf & 1) != 0).astype(int) + ((gf & 2) != 0))),
-                                 first_bad=np.flatnonzero(hit_bad | nee_bad)[:4].tolist()))
+                                 first_bad=[(int(p), (int(gt[p]), int(gp[p]), float(gtt[p]), int(gnee[p])),
+                                             (int(ot[b][p]), int(op[b][p]), float(ott[b][p]), int(onee[b][p])))
+                                            for p in bad]))
     finally:
         c.close()
     return rows

@@ -107,7 +107,7 @@ int main(int argc, char** argv) {
   a.slots = uint32_t(S);
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
-  const bool vol = d.has_volumes != 0 || d.n_circles > 0, envis = d.env.valid && d.env.use_is;
+  const bool vol = d.has_volumes != 0 || d.n_circles > 0 || d.dfs_order != 0, envis = d.env.valid && d.env.use_is;
 #define RUNQ(V, H, F)                                                  \
   do {                                                                 \
     if (d.quant_nodes) run<V, H, F, true>(d, cam, a, spp, spb, E.max_depth, out.data()); \
