@@ -114,15 +114,42 @@ int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
   } while (0)
 
+#ifdef RTG_GUARD
+// Diagnostic builds: every scratch buffer is followed by kCanary bytes of a
+// known pattern, checked after each render (guard_canaries): a store past
+// the end of an allocation whose indices were in range for what the kernels
+// were told (an undersized buffer) shows up there, which no index check can
+// see.
+constexpr size_t kCanary = 16384;
+constexpr unsigned char kCanaryByte = 0xA5;
+#endif
+
 int ensure(rt_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.p) return RT_OK;
   if (b.p) { (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
   if (bytes == 0) bytes = 16;
+#ifdef RTG_GUARD
+  hipError_t e = hipMalloc(&b.p, bytes + kCanary);
+  if (e == hipSuccess) e = hipMemset(static_cast<char*>(b.p) + bytes, kCanaryByte, kCanary);
+#else
   hipError_t e = hipMalloc(&b.p, bytes);
+#endif
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc");
   b.bytes = bytes;
   return RT_OK;
 }
+
+#ifdef RTG_GUARD
+// Number of canary bytes of `b` that no longer hold the pattern (blocks).
+size_t canary_damage(const DevBuf& b) {
+  if (!b.p) return 0;
+  std::vector<unsigned char> h(kCanary);
+  if (hipMemcpy(h.data(), static_cast<const char*>(b.p) + b.bytes, kCanary, hipMemcpyDeviceToHost) != hipSuccess) return kCanary;
+  size_t bad = 0;
+  for (unsigned char c : h) bad += c != kCanaryByte;
+  return bad;
+}
+#endif
 
 // Copies `v` to a new device buffer with room for `extra` more elements and
 // kSceneSlack bytes past them: the traversal reads a record as whole 16-B
@@ -280,7 +307,11 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // Msamples/s, and the 1/8 shards gain more.
   uint64_t tile_px = 0;
   for (const int4& tl : tiles) tile_px += uint64_t(tl.z) * uint64_t(tl.w);
-  const int auto_twins = tile_px * uint64_t(std::max(1, p->samples_per_pixel)) > kThreeTwinSamples ? 3 : kDefaultTwins;
+  // Scenes whose shading runs the lifted volumes' tests (SHADE_VOL: C3's fog)
+  // render fastest on one stream: CornellBoxScene 600x600x1000 one / two /
+  // three parts 1605 / 1563 / 1557 Msamples/s (round 4).
+  const int auto_twins = ctx->dscene.shade_kind == SHADE_VOL ? 1
+                         : tile_px * uint64_t(std::max(1, p->samples_per_pixel)) > kThreeTwinSamples ? 3 : kDefaultTwins;
   const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : auto_twins;
   const int nt = int(std::max<size_t>(1, std::min<size_t>(size_t(want_twins), tiles.size())));
   std::vector<uint32_t>& px = ctx->pix_host;
@@ -325,7 +356,13 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // CNT_WORDS_Q queue counters plus two job words per slot: room for
   // kMaxTwins twins' counters whatever `nt` this render uses (S_t sum to
   // nslots over the twins).
-  const size_t wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
+  size_t wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
+#ifdef RTG_GUARD
+  // RTGPU_GUARD_OLD_WQ=1 (diagnostic builds only): the round-3 sizing (two
+  // twins' counters), to show what its overflow does
+  static const bool old_wq = getenv("RTGPU_GUARD_OLD_WQ") && atoi(getenv("RTGPU_GUARD_OLD_WQ")) > 0;
+  if (old_wq) wq_bytes = (nslots * 2 + 2 * size_t(CNT_WORDS_Q)) * sizeof(uint32_t);
+#endif
   if (ctx->wslots < nslots) {
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
@@ -411,12 +448,16 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     a.spill_cap = spill_cap;
     a.spill = static_cast<uint32_t*>(ctx->wspill.p) + size_t(t) * spill_words;
     a.slots = uint32_t(S);
+    a.out_pixels = uint32_t(dc.width) * uint32_t(dc.height);
     ctx->twin_args[t] = a;
   }
   // the twins' slices must lie inside the batch buffers (an internal error
   // otherwise: nothing is launched)
   const size_t f4_used = size_t(fbase - static_cast<float4*>(ctx->wstate.p)) * sizeof(float4);
   const size_t q_used = size_t(qbase - static_cast<uint32_t*>(ctx->wq.p)) * sizeof(uint32_t);
+#ifdef RTG_GUARD
+  if (!old_wq)
+#endif
   if (f4_used > ctx->wstate.bytes || q_used > ctx->wq.bytes || q_used > wq_bytes)
     return set_err(ctx, RT_ERR_INVALID, "internal: twin buffers exceed the batch allocation");
   ctx->num_twins = nt;
@@ -503,6 +544,12 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     unsigned int gr[4] = {0, 0, 0, 0};
     HIPCHK(guard_report(gr));
     if (gr[0]) fprintf(stderr, "RTG_GUARD: %u bad indices, first at site %u: index %u >= length %u\n", gr[0], gr[1], gr[2], gr[3]);
+    const struct { const char* name; const DevBuf* b; } bufs[] = {
+        {"wstate", &ctx->wstate}, {"wq", &ctx->wq}, {"wpix", &ctx->wpix}, {"wacc", &ctx->wacc},
+        {"wspill", &ctx->wspill}, {"counters", &ctx->counters}, {"accum", &ctx->accum}, {"frame", &ctx->frame}};
+    for (const auto& x : bufs)
+      if (const size_t bad = canary_damage(*x.b))
+        fprintf(stderr, "RTG_GUARD: %zu canary bytes past %s (%zu bytes) overwritten (%d twins)\n", bad, x.name, x.b->bytes, nt);
   }
 #endif
   if (count || ms) {

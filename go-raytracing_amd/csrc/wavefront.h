@@ -50,6 +50,7 @@ struct WaveArgs {
   uint32_t spill_lanes;
   int32_t spill_cap;
   uint32_t slots;   // capacity of every per-slot array (RTG_GUARD bounds checks)
+  uint32_t out_pixels;  // pixels of the output frame (RTG_GUARD: k_finalize's scattered store)
 };
 
 // Queue counters, each on its own 128-B line (same-line atomics serialise);

@@ -254,6 +254,10 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
   }
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
+#ifdef RTG_GUARD
+  // every lane's spill column (TStack::spill_at) inside the spill area
+  if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(60, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
+#endif
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
                  a.spill_cap};
   Cnt cnt = {};
@@ -703,6 +707,9 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
     for (uint32_t k = 0; k < kSegs; ++k) zero_c[k * kSegStride] = 0u;
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
+#ifdef RTG_GUARD
+  if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(61, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
+#endif
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
                  a.spill_cap};
   Cnt cnt = {};
@@ -789,16 +796,17 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
-    const uint32_t flags = ldnt(&a.sj_info[k]) & 0xFFu, vis = ldnt(&a.sj_vis[k]);
+    const uint32_t kk = GIX(k, a.slots, 59);
+    const uint32_t flags = ldnt(&a.sj_info[kk]) & 0xFFu, vis = ldnt(&a.sj_vis[kk]);
     if ((flags & vis & 3u) == 0u) continue;
-    const float4 ea = ldnt(&a.ne_a[k]);
+    const float4 ea = ldnt(&a.ne_a[kk]);
     float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
     const float4 L4 = ldnt(Lp);
     V3 L;
     if (kEnvIS) {
-      const float4 pb = ldnt(&a.ne_beta[k]);
+      const float4 pb = ldnt(&a.ne_beta[kk]);
       V3 direct = mk(0.0f, 0.0f, 0.0f);
-      if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[k]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+      if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[kk]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
       if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
       L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
     } else {
@@ -824,7 +832,7 @@ __global__ __launch_bounds__(256) void k_accum(WaveArgs a, uint32_t nsamp) {
 __global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int accumulate) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x; pi < a.npix; pi += gs) {
-    float* o = out + size_t(a.pixels[pi]) * 3;
+    float* o = out + size_t(GIX(a.pixels[pi], a.out_pixels, 58)) * 3;
     double sx = a.acc[size_t(pi) * 3], sy = a.acc[size_t(pi) * 3 + 1], sz = a.acc[size_t(pi) * 3 + 2];
     if (accumulate) { sx += double(o[0]); sy += double(o[1]); sz += double(o[2]); }
     o[0] = float(sx); o[1] = float(sy); o[2] = float(sz);

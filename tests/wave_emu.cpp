@@ -105,6 +105,7 @@ int main(int argc, char** argv) {
   a.spill_lanes = 1;
   a.spill_cap = kStackMax - kRing;
   a.slots = uint32_t(S);
+  a.out_pixels = uint32_t(npix);
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
   const bool vol = d.has_volumes != 0 || d.n_circles > 0 || d.dfs_order != 0, envis = d.env.valid && d.env.use_is;
