@@ -995,6 +995,10 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
     free_scene(ctx);
     return rc;
   }
+  // the lifted volumes as DVolRec records (k_shade keeps them in LDS)
+  d.vol_recs = nullptr;
+  const std::vector<DVolRec> vrecs = build_vol_recs(h);
+  if (!vrecs.empty() && (rc = upload_vec(ctx, vrecs, &d.vol_recs))) { free_scene(ctx); return rc; }
   build_inst_entries(h);   // BLAS roots are final now
   if ((rc = upload_vec(ctx, h.inst_entries, &d.inst_entry))) { free_scene(ctx); return rc; }
   // every copy and upload kernel has landed before the scene is used (by

@@ -243,6 +243,23 @@ struct alignas(16) DVolRef {
   int32_t pad;
 };
 
+// A lifted volume whose boundary is one leaf of at most kVolRecQuads quads
+// under its wrapper chain (a Box, primitives.go: the fog of CornellBoxScene,
+// cornell-smoke's boxes), gathered into one record: the ref, the volume, the
+// boundary's DInstance and its quads, so a volume test reads one contiguous
+// record (it used to chase vol_refs -> volumes -> instances -> blas ->
+// leaves -> quads).  Built at flatten time (build_vol_recs); a scene lifts its
+// volumes only when every one has a record.  The arithmetic is volume_hit's.
+constexpr int kVolRecQuads = 6;
+constexpr int kVolRecMax = 8;     // lifted volumes a scene may have
+struct alignas(16) DVolRec {
+  DInstance inst;                 // the boundary's wrapper chain (to_object)
+  DVolume vol;
+  DVolRef ref;
+  int32_t nq, pad[3];             // quads of the boundary leaf, in leaf order
+  DQuad q[kVolRecQuads];
+};
+
 struct alignas(16) DMaterial {
   int32_t kind;              // rt_material_kind
   int32_t tex;
@@ -328,6 +345,7 @@ struct DScene {
   const DBvh* blas;
   const DVolume* volumes;
   const DVolRef* vol_refs;     // volumes lifted out of the world BVH (k_shade tests them)
+  const DVolRec* vol_recs;      // the lifted volumes' records (vol_refs order; null: none lifted)
   const DMaterial* materials;
   const DTexture* textures;
   const DLight* lights;

@@ -417,6 +417,30 @@ __device__ __forceinline__ bool rtg_lead() { return __lane_id() == uint32_t(__ff
 #else
 #define RTG_VOLUME_ATTR
 #endif
+// The end of Volume.Hit (volume.go:56-79) once the boundary's two closest
+// distances are known: clamp to the ray interval, the free flight
+// -(1/rho) ln U from the largest of the leaf's `ntests` draws, the hit.
+__device__ __forceinline__ bool volume_flight(const DVolume& vol, V3 wd, bool h1, bool h2, float t1, float t2,
+                                              float tmin, float tmax, int ntests, uint32_t key, uint32_t bounce,
+                                              uint32_t dom, float& t_out) {
+  if (!h1 || !h2) return false;
+  if (t1 < tmin) t1 = tmin;
+  if (t2 > tmax) t2 = tmax;
+  if (t1 >= t2) return false;
+  if (t1 < 0.0f) t1 = 0.0f;
+  float rl = len(wd);
+  float dist = (t2 - t1) * rl;
+  float u = 0.0f;
+  for (int p = 0; p < ntests; ++p) {
+    float up = rnd(key, ctr(bounce, dom, uint32_t(vol.vol_id) * 4u + uint32_t(p)));
+    u = up > u ? up : u;
+  }
+  float hd = vol.neg_inv_density * rt_logf(u);
+  if (hd > dist) return false;
+  t_out = t1 + hd / rl;
+  return true;
+}
+
 template <bool kCount>
 __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, float time,
                            float tmin, float tmax, int ntests, uint32_t key, uint32_t bounce,
@@ -491,22 +515,38 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
     else { h2 = found; t2 = closest; }
   }
   if (kCount) cnt.vol++;
-  if (!h1 || !h2) return false;
-  if (t1 < tmin) t1 = tmin;
-  if (t2 > tmax) t2 = tmax;
-  if (t1 >= t2) return false;
-  if (t1 < 0.0f) t1 = 0.0f;
-  float rl = len(wd);
-  float dist = (t2 - t1) * rl;
-  float u = 0.0f;
-  for (int p = 0; p < ntests; ++p) {
-    float up = rnd(key, ctr(bounce, dom, uint32_t(vol.vol_id) * 4u + uint32_t(p)));
-    u = up > u ? up : u;
+  return volume_flight(vol, wd, h1, h2, t1, t2, tmin, tmax, ntests, key, bounce, dom, t_out);
+}
+
+// volume_hit on a DVolRec record (a boundary leaf of <= kVolRecQuads
+// quads): volume_hit's cached branch operation for operation, so the same
+// bits.
+template <bool kCount>
+__device__ __forceinline__ bool volume_hit_rec(const DVolRec& V, V3 wo, V3 wd, float tmin, float tmax, int ntests,
+                                               uint32_t key, uint32_t bounce, uint32_t dom, float& t_out, Cnt& cnt) {
+  V3 o = wo, d = wd;
+  to_object(V.inst, o, d);
+  float t1 = __builtin_inff(), t2 = __builtin_inff();
+  bool h1 = false, h2 = false;
+  float tq[kVolRecQuads];
+  uint32_t valid = 0u;
+  const float ninf = -__builtin_inff();
+  for (int k = 0; k < kVolRecQuads; ++k) {
+    tq[k] = 0.0f;
+    if (k >= V.nq) continue;
+    if (quad_t(V.q[k], o, d, ninf, tq[k])) valid |= 1u << k;
   }
-  float hd = vol.neg_inv_density * rt_logf(u);
-  if (hd > dist) return false;
-  t_out = t1 + hd / rl;
-  return true;
+  for (int pass = 0; pass < 2; ++pass) {
+    const float lo = pass == 0 ? ninf : t1 + 0.0001f;
+    float closest = __builtin_inff();
+    bool found = false;
+    for (int k = 0; k < kVolRecQuads; ++k)
+      if (((valid >> k) & 1u) && lo <= tq[k] && tq[k] <= closest) { closest = tq[k]; found = true; }
+    if (pass == 0) { h1 = found; t1 = closest; if (!h1) break; }
+    else { h2 = found; t2 = closest; }
+  }
+  if (kCount) cnt.vol++;
+  return volume_flight(V.vol, wd, h1, h2, t1, t2, tmin, tmax, ntests, key, bounce, dom, t_out);
 }
 
 // Volumes lifted out of the world BVH (DVolRef): Volume.Hit (volume.go:34-79)
@@ -515,14 +555,16 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
 // miss; ht; instance; TLAS ref position) by the accept rule: closer, or on an
 // exact tie the reference's DFS order.  k_shade's volume variant and the
 // path probe (probe.hip) both call this.
+// `recs`: the volumes' DVolRec records (DScene.vol_recs: a scene lifts its
+// volumes only when every one has a record, flatten_scene).
 template <bool kCount>
-__device__ __forceinline__ void lifted_volumes(const DScene& sc, V3 ro, V3 rd, float time, uint32_t key, uint32_t bounce,
-                                               uint32_t& kh, float& ht, int& hinst, int& hrefpos, Cnt& cnt) {
+__device__ __forceinline__ void lifted_volumes(const DScene& sc, V3 ro, V3 rd, uint32_t key, uint32_t bounce,
+                                               uint32_t& kh, float& ht, int& hinst, int& hrefpos, Cnt& cnt,
+                                               const DVolRec* recs) {
   for (int v = 0; v < sc.num_vol_refs; ++v) {
-    const DVolRef vr = sc.vol_refs[v];
+    const DVolRef vr = recs[v].ref;
     float tv = 0.0f;
-    if (!volume_hit<kCount>(sc, sc.volumes[GIX(vr.vol, sc.n_volumes, 56)], ro, rd, time, 0.001f, __builtin_inff(),
-                            vr.ntests, key, bounce, DOM_VOL, tv, cnt))
+    if (!volume_hit_rec<kCount>(recs[v], ro, rd, 0.001f, __builtin_inff(), vr.ntests, key, bounce, DOM_VOL, tv, cnt))
       continue;
     if (kh == 0u || tv < ht || (tv == ht && tie_wins(sc, PK_VOLUME, vr.refpos, 0, int(kh >> 28), hrefpos, 0))) {
       kh = (uint32_t(PK_VOLUME) << 28) | uint32_t(vr.vol);

@@ -1370,10 +1370,58 @@ void build_inst_entries(HostScene& S) {
   }
 }
 
+std::vector<DVolRec> build_vol_recs(const HostScene& h) {
+  std::vector<DVolRec> recs;
+  if (h.vol_refs.empty() || h.vol_refs.size() > size_t(kVolRecMax)) return recs;
+  for (const DVolRef& vr : h.vol_refs) {
+    const DVolume& vol = h.volumes[size_t(vr.vol)];
+    const DInstance& in = h.instances[size_t(vol.boundary)];
+    const DBvh& bb = h.blas[size_t(in.blas)];
+    // volume_hit reads the boundary BLAS's root as one leaf
+    if ((bb.root_item >> ITEM_SHIFT) != ITEM_LEAF) return {};
+    const DLeaf& lf = h.leaves[bb.root_item & ITEM_MASK];
+    const int n = leaf_count(lf.info), kind = leaf_kind(lf.info);
+    if (n > kVolRecQuads) return {};
+    DVolRec r{};
+    r.inst = in;
+    r.vol = vol;
+    r.ref = vr;
+    r.nq = n;
+    for (int k = 0; k < n; ++k) {
+      int pk = kind;
+      uint32_t pi = lf.first + uint32_t(k);
+      if (kind == PK_MIXED) {
+        const uint32_t ref = h.refs[pi];
+        pk = int(ref >> REF_SHIFT);
+        pi = ref & REF_MASK;
+      }
+      if (pk != PK_QUAD) return {};
+      r.q[k] = h.quads[pi];
+    }
+    recs.push_back(r);
+  }
+  return recs;
+}
+
 int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err, const FlattenOptions& opt) {
   out = HostScene{};
-  Flattener f(desc, out, err, opt);
-  return f.run();
+  int rc;
+  {
+    Flattener f(desc, out, err, opt);
+    rc = f.run();
+  }
+  if (rc == RT_OK && !out.vol_refs.empty() && build_vol_recs(out).empty()) {
+    // k_shade tests lifted volumes through their DVolRec records only: a
+    // volume whose boundary has none (not one leaf of <= 6 quads) stays in
+    // the world BVH, where the traversal's volume variant tests it
+    FlattenOptions o = opt;
+    o.lift_volumes = 0;
+    out = HostScene{};
+    err.clear();
+    Flattener f(desc, out, err, o);
+    rc = f.run();
+  }
+  return rc;
 }
 
 }  // namespace rtg

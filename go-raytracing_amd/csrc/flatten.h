@@ -91,6 +91,11 @@ struct FlattenOptions {
 // the device BLAS builds).
 void build_inst_entries(HostScene& S);
 
+// The lifted volumes as DVolRec records (k_shade, the path probe) when every
+// boundary is one leaf of at most kVolRecQuads quads and there are at most
+// kVolRecMax of them; else empty.  Call once the BLAS roots are final.
+std::vector<DVolRec> build_vol_recs(const HostScene& S);
+
 // Returns RT_OK or an rt_status; `err` receives a message.
 int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err,
                   const FlattenOptions& opt = FlattenOptions());

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void path_hits_kernel(DScene sc, DCamera cam, 
   float ht = h.x;
   int hinst = int(__float_as_uint(h.z)), hrefpos = int(__float_as_uint(h.w));
   Cnt cnt = {};
-  if (sc.num_vol_refs > 0) lifted_volumes<false>(sc, ro, rd, ray_time(key), key, uint32_t(bounce), kh, ht, hinst, hrefpos, cnt);
+  if (sc.num_vol_refs > 0) lifted_volumes<false>(sc, ro, rd, key, uint32_t(bounce), kh, ht, hinst, hrefpos, cnt, sc.vol_recs);
   int top = -1, prim = -1;
   if (kh != 0u) hit_ids(sc, int(kh >> 28), int(kh & 0x0FFFFFFFu), hrefpos, top, prim);
   const uint32_t p = pixels[slot % npix];

@@ -29,6 +29,7 @@ struct EmuScene {
   HostScene h;
   std::vector<DNodeQ> qnodes;   // quantised nodes (build.hip k_quantize, same function)
   std::vector<DTriShade> tri_shade;   // shading records (build.hip k_tri_shade, same function)
+  std::vector<DVolRec> vol_recs;        // the lifted volumes' records (api.cpp upload_one, same function)
   DScene d{};
   DCamera cam{};
   int max_depth = 0;
@@ -108,6 +109,8 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.num_vol_refs = int32_t(h.vol_refs.size());
   d.has_volumes = h.volumes.size() > h.vol_refs.size() ? 1 : 0;
   if (d.num_vol_refs > 0) d.shade_kind = SHADE_VOL;
+  E.vol_recs = build_vol_recs(h);
+  d.vol_recs = E.vol_recs.empty() ? nullptr : E.vol_recs.data();
 
   const rt_camera_desc* c = rts_scene_get_camera(E.scn);
   DCamera& cam = E.cam;

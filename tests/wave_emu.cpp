@@ -70,9 +70,11 @@ int main(int argc, char** argv) {
   const uint32_t npix = uint32_t(cam.width) * uint32_t(cam.height);
   const size_t S = size_t(spb) * npix;
 
-  // exactly-sized buffers (the layout of render_wave in api.cpp)
-  std::vector<float4> f4(size_t(kSlotF4) * S, float4{0.0f, 0.0f, 0.0f, 0.0f});
-  std::vector<uint32_t> q(CNT_WORDS_Q + 2 * S, 0u);
+  // exactly-sized buffers, one allocation per array (render_wave in api.cpp
+  // carves the same arrays out of one buffer; separate ones let ASan see a
+  // store that leaves its array)
+  std::vector<std::vector<float4>> f4(kSlotF4, std::vector<float4>(S, float4{0.0f, 0.0f, 0.0f, 0.0f}));
+  std::vector<uint32_t> q(CNT_WORDS_Q, 0u), sj_info(S, 0u), sj_vis(S, 0u);
   std::vector<uint32_t> pixels(npix);
   // bucket-like pixel list: reversed, so slot -> pixel is not the identity
   for (uint32_t i = 0; i < npix; ++i) pixels[i] = npix - 1u - i;
@@ -82,17 +84,14 @@ int main(int argc, char** argv) {
   int err = 0;
 
   WaveArgs a{};
-  float4* base = f4.data();
-  for (int k = 0; k < 2; ++k) {
-    float4* sb = base + size_t(3 * k) * S;
-    a.s[k] = PathStream{sb, sb + S, sb + 2 * S};
-  }
-  a.hit = base + 6 * S; a.Lout = base + 7 * S;
-  a.sj_p = base + 8 * S; a.sj_a = base + 9 * S; a.sj_h = base + 10 * S;
-  a.ne_a = base + 11 * S; a.ne_h = base + 12 * S; a.ne_beta = base + 13 * S;
+  auto arr = [&](int k) { return f4[size_t(k)].data(); };
+  for (int k = 0; k < 2; ++k) a.s[k] = PathStream{arr(3 * k), arr(3 * k + 1), arr(3 * k + 2)};
+  a.hit = arr(6); a.Lout = arr(7);
+  a.sj_p = arr(8); a.sj_a = arr(9); a.sj_h = arr(10);
+  a.ne_a = arr(11); a.ne_h = arr(12); a.ne_beta = arr(13);
   a.counts = q.data();
-  a.sj_info = q.data() + CNT_WORDS_Q;
-  a.sj_vis = a.sj_info + S;
+  a.sj_info = sj_info.data();
+  a.sj_vis = sj_vis.data();
   a.pixels = pixels.data();
   a.npix = npix;
   a.acc = acc.data();
