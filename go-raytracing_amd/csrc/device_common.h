@@ -518,9 +518,61 @@ __device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol,
   return volume_flight(vol, wd, h1, h2, t1, t2, tmin, tmax, ntests, key, bounce, dom, t_out);
 }
 
+// Quad.Hit (quad_t) for an axis-aligned quad: n and w nonzero only on axis
+// K, u only on axis I and v only on axis J ({I, J} the other two; kUI: I =
+// K+1, J = K+2 cyclically, else swapped), all finite.  Every term quad_t
+// forms with a zero component is a signed zero (the ray and the record are
+// finite, and |denom| >= 1e-8 keeps tt and the hit point finite), and adding
+// a signed zero to a value leaves it unchanged, so dot(n, d) = n_K d_K,
+// dot(n, o) = n_K o_K, alpha = w_K (ph_I v_J) or w_K (-(ph_J v_I)), beta =
+// w_K (u_I ph_J) or w_K (-(u_J ph_I)): the same bits for tt and the same
+// decisions (a zero's sign never changes a comparison with 0 or 1), with a
+// third of the operations.
+template <int K, bool kUI>
+__device__ __forceinline__ bool quad_t_aa(const DQuad& q, V3 o, V3 d, float tmin, float& t) {
+  constexpr int I = (K + 1) % 3, J = (K + 2) % 3;   // cyclic successors of K
+  auto c = [](V3 v, int a) { return a == 0 ? v.x : a == 1 ? v.y : v.z; };
+  const float nk = K == 0 ? q.nx : K == 1 ? q.ny : q.nz;
+  const float wk = K == 0 ? q.wx : K == 1 ? q.wy : q.wz;
+  const float denom = nk * c(d, K);
+  if (fabsf(denom) < 1e-8f) return false;
+  const float tt = (q.D - nk * c(o, K)) / denom;
+  if (!(tmin <= tt)) return false;
+  const float phI = (c(o, I) + tt * c(d, I)) - (I == 0 ? q.Qx : I == 1 ? q.Qy : q.Qz);
+  const float phJ = (c(o, J) + tt * c(d, J)) - (J == 0 ? q.Qx : J == 1 ? q.Qy : q.Qz);
+  float alpha, beta;
+  if (kUI) {   // u on I, v on J
+    const float vJ = J == 0 ? q.vx : J == 1 ? q.vy : q.vz, uI = I == 0 ? q.ux : I == 1 ? q.uy : q.uz;
+    alpha = wk * (phI * vJ);
+    beta = wk * (uI * phJ);
+  } else {     // u on J, v on I
+    const float vI = I == 0 ? q.vx : I == 1 ? q.vy : q.vz, uJ = J == 0 ? q.ux : J == 1 ? q.uy : q.uz;
+    alpha = wk * (-(phJ * vI));
+    beta = wk * (-(uJ * phI));
+  }
+  if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
+  t = tt;
+  return true;
+}
+// A record quad: the axis-aligned form its code (DQuad::pad0 bits, set by
+// the flattener's quad_axis_code: 0x80 | K | kUI << 2) names, else quad_t.
+// The code is the same on every lane (the record is the wave's), so the
+// switch is a scalar branch.
+__device__ __forceinline__ bool quad_t_rec(const DQuad& q, V3 o, V3 d, float tmin, float& t) {
+  switch (__float_as_uint(q.pad0)) {
+    case 0x80u: return quad_t_aa<0, false>(q, o, d, tmin, t);
+    case 0x84u: return quad_t_aa<0, true>(q, o, d, tmin, t);
+    case 0x81u: return quad_t_aa<1, false>(q, o, d, tmin, t);
+    case 0x85u: return quad_t_aa<1, true>(q, o, d, tmin, t);
+    case 0x82u: return quad_t_aa<2, false>(q, o, d, tmin, t);
+    case 0x86u: return quad_t_aa<2, true>(q, o, d, tmin, t);
+    default: return quad_t(q, o, d, tmin, t);
+  }
+}
+
 // volume_hit on a DVolRec record (a boundary leaf of <= kVolRecQuads
-// quads): volume_hit's cached branch operation for operation, so the same
-// bits.
+// quads): volume_hit's cached branch operation for operation (quad_t_rec
+// gives quad_t's bits), so the same bits.
 template <bool kCount>
 __device__ __forceinline__ bool volume_hit_rec(const DVolRec& V, V3 wo, V3 wd, float tmin, float tmax, int ntests,
                                                uint32_t key, uint32_t bounce, uint32_t dom, float& t_out, Cnt& cnt) {
@@ -534,7 +586,7 @@ __device__ __forceinline__ bool volume_hit_rec(const DVolRec& V, V3 wo, V3 wd, f
   for (int k = 0; k < kVolRecQuads; ++k) {
     tq[k] = 0.0f;
     if (k >= V.nq) continue;
-    if (quad_t(V.q[k], o, d, ninf, tq[k])) valid |= 1u << k;
+    if (quad_t_rec(V.q[k], o, d, ninf, tq[k])) valid |= 1u << k;
   }
   for (int pass = 0; pass < 2; ++pass) {
     const float lo = pass == 0 ? ninf : t1 + 0.0001f;
@@ -955,6 +1007,9 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
 #if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
       asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));   // as above
+#endif
+#ifdef RTG_EXTRA_LOAD   // diagnostic: one more 16-B load per node step (the node's unused last row)
+      { const float4 x = ldn(nb + 112u); asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w)); }
 #endif
 #ifdef RTG_STAMP
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

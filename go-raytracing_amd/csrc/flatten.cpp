@@ -1370,6 +1370,26 @@ void build_inst_entries(HostScene& S) {
   }
 }
 
+// volume_hit_rec's axis-aligned quad form (device_common.h quad_t_aa): the
+// normal, u, v and w each have one nonzero component, n and w on axis k, u
+// and v on the other two.  Code: 0x80 | k | u-on-axis-(k+1) << 2; 0 = a
+// general quad.
+uint32_t quad_axis_code(const DQuad& q) {
+  const float n[3] = {q.nx, q.ny, q.nz}, u[3] = {q.ux, q.uy, q.uz}, v[3] = {q.vx, q.vy, q.vz}, w[3] = {q.wx, q.wy, q.wz};
+  auto axis = [](const float* x) {   // the one nonzero finite component, else -1
+    int a = -1;
+    for (int c = 0; c < 3; ++c) {
+      if (!std::isfinite(x[c])) return -1;
+      if (x[c] != 0.0f) { if (a >= 0) return -1; a = c; }
+    }
+    return a;
+  };
+  const int k = axis(n), iu = axis(u), iv = axis(v), iw = axis(w);
+  if (k < 0 || iw != k || iu < 0 || iv < 0 || iu == k || iv == k || iu == iv) return 0u;
+  if (!std::isfinite(q.Qx) || !std::isfinite(q.Qy) || !std::isfinite(q.Qz) || !std::isfinite(q.D)) return 0u;
+  return 0x80u | uint32_t(k) | (iu == (k + 1) % 3 ? 4u : 0u);
+}
+
 std::vector<DVolRec> build_vol_recs(const HostScene& h) {
   std::vector<DVolRec> recs;
   if (h.vol_refs.empty() || h.vol_refs.size() > size_t(kVolRecMax)) return recs;
@@ -1397,6 +1417,7 @@ std::vector<DVolRec> build_vol_recs(const HostScene& h) {
       }
       if (pk != PK_QUAD) return {};
       r.q[k] = h.quads[pi];
+      r.q[k].pad0 = __builtin_bit_cast(float, quad_axis_code(r.q[k]));
     }
     recs.push_back(r);
   }

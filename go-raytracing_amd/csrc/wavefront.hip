@@ -396,9 +396,11 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
 #endif
 // The volume variant (the material one + the lifted volumes' tests): C3
 // CornellBoxScene at 4 / 5 / 7 waves 1390 / 1454 / 1427 Msamples/s (110 / 96
-// / 72 VGPRs; 0 / 3 / 71 spilled).
+// / 72 VGPRs; 0 / 3 / 71 spilled); with the volume records (DVolRec, round
+// 4) 4 / 5 / 6 waves 1580 / 1648 / 1660 (101 / 96 / 80 VGPRs; 0 / 0 / 13
+// spilled).
 #ifndef RTG_SHADE_VOL_WAVES
-#define RTG_SHADE_VOL_WAVES 5
+#define RTG_SHADE_VOL_WAVES 6
 #endif
 #define RTG_SHADE_WAVES_FOR(kShade)                                                       \
   ((kShade) == SHADE_FULL ? RTG_SHADE_WAVES : (kShade) == SHADE_MAT ? RTG_SHADE_MAT_WAVES \
