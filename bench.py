@@ -80,6 +80,8 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dealing", choices=["static", "dynamic"], default="static",
+                    help="N > 1: tiles dealt round-robin (static) or claimed in runs as ranks / devices finish")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="cornell-lucy")
@@ -250,6 +252,12 @@ class Dist:
             dist.init_process_group(self.backend)
             self.dist = dist
 
+    def store(self):
+        """The process group's key-value store (torchrun's TCPStore): its add()
+        is atomic across ranks, the shared counter of dynamic dealing."""
+        from torch.distributed import distributed_c10d
+        return distributed_c10d._get_default_store()
+
     def barrier(self):
         if self.dist is not None:
             self.dist.barrier()
@@ -274,11 +282,35 @@ class Dist:
                 accum.copy_(host)
 
 
+def dynamic_runs(add, ntiles: int, world: int, first_pct: int = 50):
+    """Runs [start, end) of the tile list this rank claims from a counter
+    shared by all ranks (`add(k)`: atomically add k, return the new value):
+    api.cpp render_dynamic's rule, bucket_renderer.go:193-213's channel across
+    processes.  A run is 1/(2 world) of the tiles left (the first one
+    first_pct % of a fair share), at least 1/16 of a fair share; a rank
+    claims its next run once its last one is rendered."""
+    fair = -(-ntiles // world)
+    min_run = max(1, fair // 16)
+    first = max(min_run, fair * first_pct // 100)
+    runs = 0
+    while True:
+        left = ntiles - add(0)
+        if left <= 0:
+            return
+        run = first if runs == 0 else max(min_run, -(-left // (2 * world)))
+        end = add(run)
+        start = end - run
+        if start >= ntiles:
+            return
+        runs += 1
+        yield start, min(end, ntiles)
+
+
 class Workload:
     """One scene resident on this rank's GPU, this rank's bucket shard."""
 
     def __init__(self, g, D: Dist, scene: str, scene_kw: dict, seed: int, blas: str, nodes: str = "fp32",
-                 devices=None):
+                 devices=None, dealing: str = "static"):
         import torch
         self.g, self.D = g, D
         t = time.time()
@@ -301,13 +333,33 @@ class Workload:
         self.buckets = g.generate_buckets(self.W, self.H, 32)
         self.params = g.make_params(self.spp, self.depth, seed=seed,
                                     buckets=g.shard_buckets(self.buckets, D.rank, D.world, SHARD_TILE))
+        # dynamic dealing: a multi-device context claims runs itself
+        # (RT_DEAL_DYNAMIC); ranks claim runs of the whole tile list through
+        # the process group's store, one counter per frame
+        self.dealing = dealing
+        if devices is not None:
+            self.ctx.set_dealing(dealing)
+        self.all_tiles = g.split_buckets(self.buckets, SHARD_TILE)
+        self.frame_no = 0
+        self.tiles_rendered = 0
         self.accum = torch.zeros(self.H * self.W * 3, dtype=torch.float32, device=D.dev)
         self.stream = torch.cuda.current_stream(D.dev)
         self.kernel_ms, self.kernel_times = [], []
 
     def step(self, timed: bool = False, kernel_timing: bool = False):
         self.accum.zero_()
-        self.ctx.render_device(self.cam, self.params, self.accum.data_ptr(), self.stream.cuda_stream)
+        if self.dealing == "dynamic" and self.D.world > 1:
+            store = self.D.store()
+            key = f"rtgpu_deal_{self.frame_no}"
+            self.frame_no += 1
+            self.tiles_rendered = 0
+            for a, b in dynamic_runs(lambda k: store.add(key, k), len(self.all_tiles), self.D.world):
+                p = self.g.make_params(self.spp, self.depth, seed=self.seed, buckets=self.all_tiles[a:b])
+                self.ctx.render_device(self.cam, p, self.accum.data_ptr(), self.stream.cuda_stream)
+                self.ctx.sync()   # the next claim follows this rank's progress
+                self.tiles_rendered += b - a
+        else:
+            self.ctx.render_device(self.cam, self.params, self.accum.data_ptr(), self.stream.cuda_stream)
         if timed:
             # blocks until the render kernel has finished; raises on a device error
             self.kernel_ms.append(self.ctx.last_render_kernel_ms())
@@ -448,7 +500,7 @@ def main():
     if D.world == 1 and args.gpus > 1:
         env_dev = os.environ.get("RTGPU_BENCH_DEVICES")
         devices = [int(x) for x in env_dev.split(",")] if env_dev else list(range(args.gpus))
-    w = Workload(g, D, args.scene, scene_kw, args.seed, args.blas, args.nodes, devices)
+    w = Workload(g, D, args.scene, scene_kw, args.seed, args.blas, args.nodes, devices, args.dealing)
     W, H, spp, depth = w.W, w.H, w.spp, w.depth
 
     # one HIP event before each extend/shade/shadow launch (and after each
@@ -558,7 +610,7 @@ def main():
                 configs[cid] = {"workload": f"{scene} {W}x{H} {spp}spp depth {depth}", "value": round(value, 3),
                                 "ms_per_step": round(ms_per_step, 3), "steps": args.steps, "frame_sum": frame_sum}
                 continue
-            cw = Workload(g, D, scene, kw, args.seed, args.blas, args.nodes, devices)
+            cw = Workload(g, D, scene, kw, args.seed, args.blas, args.nodes, devices, args.dealing)
             el = cw.run(args.config_steps, 1)
             configs[cid] = {"workload": f"{scene} {cw.W}x{cw.H} {cw.spp}spp depth {cw.depth}",
                             "value": round(cw.samples() * args.config_steps / el / 1e6, 3),
@@ -627,13 +679,20 @@ def main():
             "data": "synthetic (deterministic 280K-tri Lucy stand-in; scene geometry per scenes.go)",
             "config": {"workload": f"{args.scene} {W}x{H} {spp}spp depth {depth}", "scene": args.scene,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "parallelism": f"tiles-rr{D.world}" if devices is None else f"ctx-multi{devices}", "buckets": len(w.buckets), "blas": args.blas, "nodes": args.nodes,
+                       "parallelism": (f"tiles-{'rr' if args.dealing == 'static' else 'dyn'}{D.world}" if devices is None
+                                       else f"ctx-multi{devices}-{args.dealing}"), "buckets": len(w.buckets), "blas": args.blas, "nodes": args.nodes,
                        "triangles": w.info.triangles, "bvh_nodes": w.info.nodes,
                        "scene_build_s": round(w.build_s, 2), "device_bvh_build_ms": round(w.dev_build_ms, 2),
                        "image_finite": img_ok, "frame_sum": frame_sum},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if args.dealing == "dynamic":
+            if devices is not None:
+                tiles, runs = w.ctx.last_dealing()
+                line["dealing"] = {"tiles_per_device": tiles, "runs_per_device": runs}
+            elif D.world > 1:
+                line["dealing"] = {"rank0_tiles": w.tiles_rendered, "tiles": len(w.all_tiles)}
         if kernels is not None:
             line["kernels"] = kernels
         if work is not None:

@@ -36,6 +36,8 @@ RT_OPT_BVH4_COLLAPSE = 9
 RT_COLLAPSE_SAH, RT_COLLAPSE_GREEDY = 0, 1
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
+RT_OPT_DEALING, RT_OPT_DEAL_FIRST = 10, 11
+RT_DEAL_STATIC, RT_DEAL_DYNAMIC = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_SCENE", -6: "RT_ERR_DEVICE"}
 
@@ -165,6 +167,8 @@ def rtgpu() -> C.CDLL:
             lib.rt_ctx_create_multi.argtypes = [C.POINTER(I32), I32, C.POINTER(P)]
             lib.rt_ctx_num_devices.argtypes = [P]
             lib.rt_device_count.argtypes = [C.POINTER(I32)]
+        if hasattr(lib, "rt_last_dealing"):
+            lib.rt_last_dealing.argtypes = [P, C.POINTER(I32), C.POINTER(I32), I32]
         lib.rt_ctx_destroy.argtypes = [P]
         lib.rt_ctx_destroy.restype = None
         lib.rt_last_error.argtypes = [P]
@@ -419,6 +423,21 @@ class Context:
     @property
     def num_devices(self) -> int:
         return int(self._lib.rt_ctx_num_devices(self._h))
+
+    def set_dealing(self, mode: str = "static", first_share: int = 0):
+        """Multi-device tile dealing (RT_OPT_DEALING): "static" (tile k to
+        device k mod n) or "dynamic" (runs claimed from a shared counter as
+        devices finish, bucket_renderer.go:193-213); first_share = the first
+        run in percent of a fair share (0: default)."""
+        self.set_option(RT_OPT_DEALING, {"static": RT_DEAL_STATIC, "dynamic": RT_DEAL_DYNAMIC}[mode])
+        self.set_option(RT_OPT_DEAL_FIRST, first_share)
+
+    def last_dealing(self):
+        """(tiles, runs) per device of the last multi-device render."""
+        n = self.num_devices
+        tiles, runs = (C.c_int32 * n)(), (C.c_int32 * n)()
+        self._check(self._lib.rt_last_dealing(self._h, tiles, runs, n))
+        return list(tiles), list(runs)
 
     def close(self):
         if getattr(self, "_h", None):

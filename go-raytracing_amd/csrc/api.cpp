@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -91,6 +92,13 @@ struct rt_ctx {
   hipEvent_t twin_off_ev = nullptr;   // twin phase offset (WavePlan::offset_ev)
   hipEvent_t fan_ev = nullptr;    // caller-stream point the devices' renders start after
   hipEvent_t join_ev = nullptr;   // end of this device's share of a render
+  // RT_OPT_DEALING: how a multi-device render deals its tiles (set on the
+  // primary; RT_DEAL_STATIC round-robin, RT_DEAL_DYNAMIC claimed runs)
+  int opt_dealing = RT_DEAL_STATIC;
+  int opt_first_share = 0;        // RT_OPT_DEAL_FIRST: first run, percent of a fair share (0 = default)
+  hipEvent_t dyn_ev0 = nullptr;   // start of this device's runs in a dynamic render
+  bool dyn_span = false;          // the last render was dynamic: its kernel span starts at dyn_ev0
+  int32_t dealt_tiles = 0, dealt_runs = 0;   // this device's share of the last multi-device render
 };
 
 namespace {
@@ -613,6 +621,9 @@ int fan_out(rt_ctx* ctx, F f) {
 int render_share(rt_ctx* ctx, rt_ctx* primary, const rt_camera_desc* cam, const rt_render_params* p,
                  const std::vector<rt_bucket>& share, float* d_out, hipStream_t caller) {
   ctx->kev_recorded = false;
+  ctx->dyn_span = false;
+  ctx->dealt_tiles = int32_t(share.size());
+  ctx->dealt_runs = share.empty() ? 0 : 1;
   if (share.empty()) return RT_OK;
   rt_render_params q = *p;
   q.buckets = share.data();
@@ -623,6 +634,69 @@ int render_share(rt_ctx* ctx, rt_ctx* primary, const rt_camera_desc* cam, const 
   int rc = render_impl(ctx, cam, &q, d_out, s, false, nullptr, nullptr);
   if (rc) return rc;
   if (!first) HIPCHK(hipEventRecord(ctx->join_ev, s));
+  return RT_OK;
+}
+
+// Dynamic dealing (RT_DEAL_DYNAMIC): the reference's worker pool fed by a
+// channel (bucket_renderer.go:193-213), one worker per device.  Each
+// device's host thread claims a run of consecutive tiles from one shared
+// counter, renders it on its own stream, waits for it, and claims again
+// until no tile is left, so a device that runs slower (clock, peer-write
+// contention) or starts later renders fewer tiles.  A run is a share of the
+// tiles left (guided self-scheduling): 1/(2n) of them, the first run
+// RT_OPT_DEAL_FIRST percent of a fair share (default 50), none smaller than
+// 1/16 of a fair share — each run is one render of its own, with its own
+// launch tails, so the runs stay few.  Each pixel is still rendered by
+// exactly one device with the same RNG keys, so the frame is bit-identical
+// to the static split's and to one device's.
+int render_dynamic(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params* p,
+                   const std::vector<rt_bucket>& tiles, float* d_out, hipStream_t st) {
+  rt_ctx* const primary = ctx;
+  const size_t n = 1 + ctx->subs.size(), T = tiles.size();
+  const size_t fair = (T + n - 1) / n;
+  const size_t min_run = std::max<size_t>(1, fair / 16);
+  const size_t first_pct = size_t(ctx->opt_first_share ? ctx->opt_first_share : 50);
+  const size_t first = std::max(min_run, fair * first_pct / 100);
+  std::atomic<size_t> next{0};
+  HIPCHK(hipEventRecord(primary->fan_ev, st));
+  int rc = fan_out(primary, [&](int, rt_ctx* c) -> int {
+    rt_ctx* ctx = c;   // HIPCHK reports on this device's context
+    c->kev_recorded = false;
+    c->dyn_span = false;
+    c->dealt_tiles = 0;
+    c->dealt_runs = 0;
+    hipStream_t s = c->stream;
+    HIPCHK(hipStreamWaitEvent(s, primary->fan_ev, 0));
+    HIPCHK(hipEventRecord(c->dyn_ev0, s));
+    for (;;) {
+      // claim [cur, cur + run): a share of what is left
+      size_t cur = next.load(std::memory_order_relaxed), run = 0;
+      do {
+        if (cur >= T) break;
+        const size_t left = T - cur;
+        run = c->dealt_runs == 0 ? first : std::max(min_run, (left + 2 * n - 1) / (2 * n));
+        run = std::min(run, left);
+      } while (!next.compare_exchange_weak(cur, cur + run, std::memory_order_relaxed));
+      if (cur >= T) break;
+      rt_render_params q = *p;
+      q.buckets = tiles.data() + cur;
+      q.num_buckets = int32_t(run);
+      const int r = render_impl(c, cam, &q, d_out, s, false, nullptr, nullptr);
+      if (r) return r;
+      c->dealt_tiles += int32_t(run);
+      c->dealt_runs += 1;
+      // the next claim follows this device's progress
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    c->dyn_span = c->dealt_runs > 0;
+    HIPCHK(hipEventRecord(c->join_ev, s));
+    return RT_OK;
+  });
+  if (rc) return rc;
+  // the caller's stream continues after every device's runs (already done:
+  // each thread waited for its last run)
+  HIPCHK(hipStreamWaitEvent(st, primary->join_ev, 0));
+  for (rt_ctx* sub : primary->subs) HIPCHK(hipStreamWaitEvent(st, sub->join_ev, 0));
   return RT_OK;
 }
 
@@ -644,6 +718,7 @@ int render_multi(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params*
     for (int y = b.y; y < b.y + b.height; y += 16)
       for (int x = b.x; x < b.x + b.width; x += 16)
         tiles.push_back({x, y, std::min(16, b.x + b.width - x), std::min(16, b.y + b.height - y)});
+  if (ctx->opt_dealing == RT_DEAL_DYNAMIC) return render_dynamic(ctx, cam, p, tiles, d_out, st);
   std::vector<std::vector<rt_bucket>> share(n);
   for (size_t i = 0; i < tiles.size(); ++i) share[i % n].push_back(tiles[i]);
   HIPCHK(hipEventRecord(ctx->fan_ev, st));
@@ -691,6 +766,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
       hipEventCreateWithFlags(&ctx->fan_ev, hipEventDisableTiming) != hipSuccess ||
       !create_twin_streams(ctx) ||
       hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&ctx->dyn_ev0) != hipSuccess ||
       hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
     delete ctx;
     return RT_ERR_HIP;
@@ -739,6 +815,16 @@ int rt_ctx_create_multi(const int32_t* devices, int32_t num_devices, rt_ctx** ou
 
 int rt_ctx_num_devices(const rt_ctx* ctx) { return ctx ? 1 + int(ctx->subs.size()) : 0; }
 
+int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t max_devices) {
+  if (!ctx || !tiles || !runs || max_devices < 0) return RT_ERR_INVALID;
+  for (int32_t k = 0; k < max_devices && k <= int32_t(ctx->subs.size()); ++k) {
+    const rt_ctx* c = k == 0 ? ctx : ctx->subs[size_t(k - 1)];
+    tiles[k] = c->dealt_tiles;
+    runs[k] = c->dealt_runs;
+  }
+  return RT_OK;
+}
+
 void rt_ctx_destroy(rt_ctx* ctx) {
   if (!ctx) return;
   for (rt_ctx* s : ctx->subs) rt_ctx_destroy(s);
@@ -769,6 +855,7 @@ void rt_ctx_destroy(rt_ctx* ctx) {
     if (ctx->twin_st[t]) { (void)hipStreamSynchronize(ctx->twin_st[t]); (void)hipStreamDestroy(ctx->twin_st[t]); }
   }
   if (ctx->join_ev) (void)hipEventDestroy(ctx->join_ev);
+  if (ctx->dyn_ev0) (void)hipEventDestroy(ctx->dyn_ev0);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -825,6 +912,16 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (key == RT_OPT_MAX_BLOCKS) {
     if (value < 0) return set_err(ctx, RT_ERR_INVALID, "bad max blocks");
     ctx->opt_blocks = value;
+    return RT_OK;
+  }
+  if (key == RT_OPT_DEALING) {
+    if (value != RT_DEAL_STATIC && value != RT_DEAL_DYNAMIC) return set_err(ctx, RT_ERR_INVALID, "bad dealing mode");
+    ctx->opt_dealing = value;
+    return RT_OK;
+  }
+  if (key == RT_OPT_DEAL_FIRST) {
+    if (value < 0 || value > 100) return set_err(ctx, RT_ERR_INVALID, "first run must be 0 (default) or 1..100 percent");
+    ctx->opt_first_share = value;
     return RT_OK;
   }
   return set_err(ctx, RT_ERR_INVALID, "unknown option " + std::to_string(key));
@@ -1112,7 +1209,8 @@ int rt_last_render_kernel_ms(rt_ctx* ctx, double* ms) {
     if (!ctx->kev_recorded) return RT_OK;
     HIPCHK(hipEventSynchronize(ctx->kev1));
     float f = 0.f;
-    HIPCHK(hipEventElapsedTime(&f, ctx->kev0, ctx->kev1));
+    // a dynamic render: from this device's first run to the end of its last
+    HIPCHK(hipEventElapsedTime(&f, ctx->dyn_span ? ctx->dyn_ev0 : ctx->kev0, ctx->kev1));
     per[size_t(k)] = f;
     return check_render_error(ctx, true);
   });

@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the RT_ABI_VERSION this binding was written against.
-const ABIVersion = 5 // RT_ABI_VERSION
+const ABIVersion = 6 // RT_ABI_VERSION
 
 // Hittable kinds (enum rt_hittable_kind).
 const (
@@ -104,6 +104,10 @@ const (
 	BuildDevice     int32 = 2 // RT_BLAS_DEVICE
 	NodesFP32       int32 = 0 // RT_NODES_FP32
 	NodesQuant8     int32 = 1 // RT_NODES_QUANT8
+	OptDealing      int32 = 10 // RT_OPT_DEALING
+	OptDealFirst    int32 = 11 // RT_OPT_DEAL_FIRST
+	DealStatic      int32 = 0  // RT_DEAL_STATIC
+	DealDynamic     int32 = 1  // RT_DEAL_DYNAMIC
 )
 
 // Node mirrors rt_hittable: one node per concrete rt.Hittable.  P holds the
@@ -330,6 +334,19 @@ func New(devices ...int) (*Ctx, error) {
 // NumDevices is the number of devices the context renders on.
 func (c *Ctx) NumDevices() int { return int(C.rt_ctx_num_devices(c.p)) }
 
+// LastDealing reports the last multi-device render's split: the tiles each
+// device rendered and the runs it claimed (rt_last_dealing).
+func (c *Ctx) LastDealing() (tiles, runs []int32, err error) {
+	n := c.NumDevices()
+	tiles, runs = make([]int32, n), make([]int32, n)
+	if n == 0 {
+		return tiles, runs, nil
+	}
+	err = c.check(C.rt_last_dealing(c.p, (*C.int32_t)(unsafe.Pointer(&tiles[0])),
+		(*C.int32_t)(unsafe.Pointer(&runs[0])), C.int32_t(n)))
+	return tiles, runs, err
+}
+
 // Close releases the context and its device memory.
 func (c *Ctx) Close() {
 	if c.p != nil {
@@ -347,7 +364,8 @@ func (c *Ctx) check(rc C.int) error {
 
 // SetOption sets a context option (OptBLASBuilder / OptTLASBuilder /
 // OptNodeFormat / OptVolumes / OptBVH4Collapse, or a schedule option: OptBatchSlots, OptRefill,
-// OptMaxBlocks, OptStreams, which never change the image).  The scene
+// OptMaxBlocks, OptStreams, OptDealing, OptDealFirst, which never change
+// the image).  The scene
 // options take effect at the next Upload, the schedule options at the next
 // render.
 func (c *Ctx) SetOption(key, value int32) error {

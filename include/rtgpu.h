@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -268,6 +268,10 @@ int rt_device_count(int32_t* num_devices);
  * device.  RT_ERR_UNSUPPORTED: a device without peer access to devices[0]. */
 int rt_ctx_create_multi(const int32_t* devices, int32_t num_devices, rt_ctx** out);
 int rt_ctx_num_devices(const rt_ctx* ctx);
+/* The last multi-device render's split: per device (in the context's device
+ * order, up to max_devices) the tiles it rendered and the runs it claimed
+ * (static dealing: one run per device with tiles).                         */
+int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t max_devices);
 
 /* Context options (take effect at the next rt_scene_upload).
  *   RT_OPT_BLAS_BUILDER: how an all-triangle mesh BVH (LoadOBJ ->
@@ -318,10 +322,25 @@ int rt_ctx_num_devices(const rt_ctx* ctx);
  *   RT_OPT_STREAMS: 1..4: the bucket tiles are dealt to that many parts
  *     ("twins"), each rendered on its own HIP stream, so one part's kernel
  *     tails overlap the others' kernels; 1 keeps one stream.  Default: 3
- *     for renders of more than 2^28 samples (pixels x spp), else 2.        */
+ *     for renders of more than 2^28 samples (pixels x spp), else 2.
+ *   RT_OPT_DEALING (multi-device contexts): how a render deals its 16x16
+ *     tiles to the devices.  RT_DEAL_STATIC (default) = tile k to device
+ *     k mod n, every share rendered at once, asynchronously.
+ *     RT_DEAL_DYNAMIC = the reference's worker pool fed by a channel
+ *     (bucket_renderer.go:193-213): each device's host thread claims runs of
+ *     consecutive tiles from one shared counter and renders each run, then
+ *     claims the next, until none are left; a run is a share of the tiles
+ *     left (guided self-scheduling), so a slower or later device takes
+ *     fewer.  The first run is RT_OPT_DEAL_FIRST percent (1..100, default
+ *     50) of a device's fair share; no run is smaller than 1/16 of one.
+ *     rt_render_device then returns once every run has been rendered (the
+ *     claims follow the devices' progress); the frame is bit-identical to
+ *     the static split's and to one device's.  rt_last_dealing reports the
+ *     split.                                                             */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7,
-       RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9 };
+       RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9, RT_OPT_DEALING = 10, RT_OPT_DEAL_FIRST = 11 };
+enum { RT_DEAL_STATIC = 0, RT_DEAL_DYNAMIC = 1 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
 enum { RT_VOLUMES_LIFTED = 0, RT_VOLUMES_IN_BVH = 1 };

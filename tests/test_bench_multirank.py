@@ -32,18 +32,19 @@ def _line(out):
 
 
 @pytest.mark.gpu
-def test_two_ranks_combine_to_the_single_rank_frame():
+@pytest.mark.parametrize("dealing", ["static", "dynamic"])
+def test_two_ranks_combine_to_the_single_rank_frame(dealing):
     env = dict(os.environ)
     one = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, env=env, capture_output=True, text=True,
                          timeout=240)
     assert one.returncode == 0, one.stderr[-3000:]
     env["RTGPU_BENCH_BACKEND"] = "gloo"
     two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2"]
-                         + ARGS, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                          "--dealing", dealing] + ARGS, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert two.returncode == 0, two.stderr[-3000:]
     a, b = _line(one.stdout), _line(two.stdout)
     assert a["n_gpus"] == 1 and b["n_gpus"] == 2
-    assert b["config"]["parallelism"] == "tiles-rr2"
+    assert b["config"]["parallelism"] == ("tiles-rr2" if dealing == "static" else "tiles-dyn2")
     assert a["config"]["image_finite"] and b["config"]["image_finite"]
     assert a["config"]["frame_sum"] == b["config"]["frame_sum"] > 0

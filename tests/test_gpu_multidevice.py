@@ -90,3 +90,49 @@ def test_multi_device_options_and_count(g):
             c.set_option(g.RT_OPT_REFILL, 99)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("devices,first", [([0, 0, 0], 0), ([0, 0], 10), ([0, 0, 0, 0], 100)])
+def test_dynamic_dealing_frame_equals_one_device(g, lucy, devices, first):
+    """RT_DEAL_DYNAMIC (bucket_renderer.go:193-213's channel): every device
+    claims runs of tiles from one counter until none are left.  Whatever the
+    split, the frame is bit-identical to one device's and to the static
+    split's, every tile is rendered exactly once, and the runs shrink as the
+    list drains (more runs than devices when the first run is a small share)."""
+    import torch
+    cam = lucy.camera
+    p = g.make_params(6, cam.max_depth, seed=13)
+    one = g.Context(0)
+    multi = g.Context(devices=devices)
+    try:
+        one.upload(lucy.desc)
+        multi.upload(lucy.desc)
+        a, _ = one.render(cam, p)
+        multi.set_dealing("static")
+        s, _ = multi.render(cam, p)
+        st_tiles, st_runs = multi.last_dealing()
+        assert np.array_equal(a, s)
+        multi.set_dealing("dynamic", first)
+        b, _ = multi.render(cam, p)
+        tiles, runs = multi.last_dealing()
+        assert np.array_equal(a, b)
+        assert sum(tiles) == sum(st_tiles) > 0 and st_runs == [1] * len(devices)
+        assert all((t > 0) == (r > 0) for t, r in zip(tiles, runs))
+        if first == 10:
+            assert sum(runs) > len(devices)
+        # the asynchronous entry point on a caller stream: same frame
+        dev = torch.device("cuda", 0)
+        buf = torch.full((cam.image_height * cam.image_width * 3,), 5.0, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)
+        cs = torch.cuda.Stream(dev)
+        with torch.cuda.stream(cs):
+            buf.zero_()
+            multi.render_device(cam, p, buf.data_ptr(), cs.cuda_stream)
+            out = buf.cpu().numpy().reshape(a.shape)
+        assert np.array_equal(out, a)
+        assert multi.last_render_kernel_ms() > 0.0
+        with pytest.raises(g.RTError):
+            multi.set_option(g.RT_OPT_DEALING, 7)
+    finally:
+        multi.close()
+        one.close()

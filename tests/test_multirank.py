@@ -92,3 +92,93 @@ def test_shards_balance_work(g):
         sizes = [len(g.shard_buckets(b, r, world)) for r in range(world)]
         assert max(sizes) - min(sizes) <= 1
         assert sum(sizes) == len(b)
+
+
+def _rank_dynamic(rank, world, port, out_path, slow_rank):
+    """bench.py's dynamic dealing across ranks: runs of the whole tile list
+    claimed through the process group's store (dynamic_runs), each rendered
+    before the next claim; slow_rank sleeps after each run, as a device with a
+    lower clock would take longer."""
+    import sys
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g, O, s = _scene()
+        if ROOT not in sys.path:
+            sys.path.insert(0, ROOT)
+        import bench
+        from torch.distributed import distributed_c10d
+        store = distributed_c10d._get_default_store()
+        cam = s.camera
+        W, H = cam.image_width, cam.image_height
+        tiles = g.split_buckets(g.generate_buckets(W, H, 32), 16)
+        frame = None
+        owner = np.zeros((H, W), np.int64)
+        runs = 0
+        for a, b in bench.dynamic_runs(lambda k: store.add("deal_test", k), len(tiles), world):
+            mine = tiles[a:b]
+            part = O.render(s.desc, cam, g.make_params(SPP, cam.max_depth, seed=SEED, buckets=mine), fp32=True,
+                            threads=2)
+            for (x, y, w, h) in mine:
+                owner[y:y + h, x:x + w] += 1
+            frame = part.copy() if frame is None else frame + part   # zero outside the run's tiles
+            runs += 1
+            if rank == slow_rank:
+                time.sleep(0.4)
+        t = torch.from_numpy(frame)
+        o = torch.from_numpy(owner)
+        n = torch.tensor([int(owner.sum()), runs], dtype=torch.int64)
+        counts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(counts, n)
+        dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+        dist.reduce(o, dst=0, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            np.save(out_path + ".frame.npy", t.numpy())
+            np.save(out_path + ".owner.npy", o.numpy())
+            np.save(out_path + ".counts.npy", torch.stack(counts).numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dynamic_dealing_across_ranks(tmp_path, g, O):
+    """Every tile is claimed by exactly one rank, the combined frame equals the
+    one-process render bit for bit, and the rank that takes longer per run
+    renders fewer pixels (bucket_renderer.go:193-213: a slow worker just
+    takes fewer buckets)."""
+    world = 2
+    out = str(tmp_path / "dyn")
+    mp.start_processes(_rank_dynamic, args=(world, _free_port(), out, 1), nprocs=world, join=True,
+                       start_method="spawn")
+    combined = np.load(out + ".frame.npy")
+    owner = np.load(out + ".owner.npy")
+    counts = np.load(out + ".counts.npy")
+    assert (owner == 1).all(), "claimed runs must partition the frame"
+    _, _, s = _scene()
+    cam = s.camera
+    full = O.render(s.desc, cam, g.make_params(SPP, cam.max_depth, seed=SEED), fp32=True, threads=4)
+    assert np.array_equal(combined, full)
+    px = counts[:, 0]
+    assert px.sum() == cam.image_width * cam.image_height
+    assert px[0] > px[1], f"the slow rank should render fewer pixels: {px.tolist()}"
+
+
+def test_dynamic_runs_rule():
+    """dynamic_runs (bench.py) on one rank: the runs tile the list in order,
+    the first is half a fair share and later ones shrink to the minimum."""
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    box = [0]
+
+    def add(k):
+        box[0] += k
+        return box[0]
+    runs = list(bench.dynamic_runs(add, 1000, 4))
+    assert runs[0] == (0, 125)
+    assert all(a == b0 for (_, a), (b0, _) in zip(runs, runs[1:])) and runs[-1][1] == 1000
+    sizes = [b - a for a, b in runs]
+    assert sizes[1] == -(-(1000 - 125) // 8) and min(sizes[:-1]) >= 250 // 16

@@ -1,0 +1,6 @@
+for rep in 1 2; do for v in prev:lib_prev new:lib; do n=${v%%:*}; l=${v##*:}
+RTGPU_LIB_DIR=$l timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs --no-pmc --no-three-pass --no-count > gpurun_out/bal_${n}_$rep.json 2> gpurun_out/bal_${n}_$rep.err || exit 1
+python3 -c "
+import json; d=json.loads(open('gpurun_out/bal_${n}_$rep.json').read().strip().splitlines()[-1]); b=d['shard_balance']
+print('$n', d['value'], b['full_frame_ms'], [(k, b[k]['predicted_speedup'], round(sum(b[k]['shard_ms']),1), b[k]['max_over_mean']) for k in ('n2','n4','n8')], flush=True)"
+done; done

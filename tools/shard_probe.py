@@ -56,9 +56,16 @@ def analyze(root):
         span = (grp[-1][1] - grp[0][0]) / 1e6
         busy = sum((e - s) for s, e, _ in grp) / 1e6
         print(f"render {gi}: {len(grp)} launches, span {span:.2f} ms, sum of durations {busy:.2f} ms")
+        per = {}
         for s, e, k in grp:
-            if k.startswith("k_"):
-                print(f"   {k:14s} {(e - s) / 1e6:8.3f} ms  gap-before {(s - grp[0][0]) / 1e6:8.3f}")
+            c = per.setdefault(k, [0, 0.0])
+            c[0] += 1
+            c[1] += (e - s) / 1e6
+        print("   " + ", ".join(f"{k} {n}x {ms:.2f}" for k, (n, ms) in sorted(per.items(), key=lambda kv: -kv[1][1])))
+        if os.environ.get("SP_LAUNCHES"):
+            for s, e, k in grp:
+                if k.startswith("k_"):
+                    print(f"   {k:14s} {(e - s) / 1e6:8.3f} ms  at {(s - grp[0][0]) / 1e6:8.3f}")
 
 
 if __name__ == "__main__":
