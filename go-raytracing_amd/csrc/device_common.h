@@ -570,23 +570,50 @@ __device__ __forceinline__ bool quad_t_rec(const DQuad& q, V3 o, V3 d, float tmi
   }
 }
 
+// Wave-uniform read-only records through the constant address space: loads
+// through such a pointer are scalar loads (s_load, the scalar cache).  Through
+// a generic pointer the compiler cannot prove the record unchanged in a
+// kernel that stores, and issues one vector load per field instead (k_shade's
+// volume variant: 94 global_load_dword for the record, every one a full
+// vector-memory instruction).
+#if defined(RTG_HOST_EMU) || !defined(__HIP_DEVICE_COMPILE__)
+#define RTG_KAS   // (the host passes of hipcc and the host emulation)
+#else
+#define RTG_KAS __attribute__((address_space(4)))
+#endif
+typedef const RTG_KAS DVolRec* KVolRec;
+__device__ __forceinline__ KVolRec kvolrec(const DVolRec* p, int v) { return (KVolRec)(p) + v; }
+
+// to_object on a record's wrapper chain, field by field
+__device__ __forceinline__ void to_object_k(const RTG_KAS DInstance* in, V3& o, V3& d) {
+  const int n = in->nwrap;
+  for (int i = 0; i < n; ++i) {
+    const int k = in->kind[i];
+    const RTG_KAS float* p = in->prm[i];
+    if (k == W_SCALE) wrap_ray3(k, p[3], p[4], p[5], o, d);
+    else wrap_ray3(k, p[0], p[1], p[2], o, d);
+  }
+}
+
 // volume_hit on a DVolRec record (a boundary leaf of <= kVolRecQuads
 // quads): volume_hit's cached branch operation for operation (quad_t_rec
 // gives quad_t's bits), so the same bits.
 template <bool kCount>
-__device__ __forceinline__ bool volume_hit_rec(const DVolRec& V, V3 wo, V3 wd, float tmin, float tmax, int ntests,
+__device__ __forceinline__ bool volume_hit_rec(KVolRec V, V3 wo, V3 wd, float tmin, float tmax, int ntests,
                                                uint32_t key, uint32_t bounce, uint32_t dom, float& t_out, Cnt& cnt) {
   V3 o = wo, d = wd;
-  to_object(V.inst, o, d);
+  to_object_k(&V->inst, o, d);
   float t1 = __builtin_inff(), t2 = __builtin_inff();
   bool h1 = false, h2 = false;
   float tq[kVolRecQuads];
   uint32_t valid = 0u;
   const float ninf = -__builtin_inff();
+  const int nq = V->nq;
   for (int k = 0; k < kVolRecQuads; ++k) {
     tq[k] = 0.0f;
-    if (k >= V.nq) continue;
-    if (quad_t_rec(V.q[k], o, d, ninf, tq[k])) valid |= 1u << k;
+    if (k >= nq) continue;
+    const DQuad q = V->q[k];
+    if (quad_t_rec(q, o, d, ninf, tq[k])) valid |= 1u << k;
   }
   for (int pass = 0; pass < 2; ++pass) {
     const float lo = pass == 0 ? ninf : t1 + 0.0001f;
@@ -598,7 +625,8 @@ __device__ __forceinline__ bool volume_hit_rec(const DVolRec& V, V3 wo, V3 wd, f
     else { h2 = found; t2 = closest; }
   }
   if (kCount) cnt.vol++;
-  return volume_flight(V.vol, wd, h1, h2, t1, t2, tmin, tmax, ntests, key, bounce, dom, t_out);
+  const DVolume vol = V->vol;
+  return volume_flight(vol, wd, h1, h2, t1, t2, tmin, tmax, ntests, key, bounce, dom, t_out);
 }
 
 // Volumes lifted out of the world BVH (DVolRef): Volume.Hit (volume.go:34-79)
@@ -614,9 +642,10 @@ __device__ __forceinline__ void lifted_volumes(const DScene& sc, V3 ro, V3 rd, u
                                                uint32_t& kh, float& ht, int& hinst, int& hrefpos, Cnt& cnt,
                                                const DVolRec* recs) {
   for (int v = 0; v < sc.num_vol_refs; ++v) {
-    const DVolRef vr = recs[v].ref;
+    const KVolRec R = kvolrec(recs, v);
+    const DVolRef vr = R->ref;
     float tv = 0.0f;
-    if (!volume_hit_rec<kCount>(recs[v], ro, rd, 0.001f, __builtin_inff(), vr.ntests, key, bounce, DOM_VOL, tv, cnt))
+    if (!volume_hit_rec<kCount>(R, ro, rd, 0.001f, __builtin_inff(), vr.ntests, key, bounce, DOM_VOL, tv, cnt))
       continue;
     if (kh == 0u || tv < ht || (tv == ht && tie_wins(sc, PK_VOLUME, vr.refpos, 0, int(kh >> 28), hrefpos, 0))) {
       kh = (uint32_t(PK_VOLUME) << 28) | uint32_t(vr.vol);

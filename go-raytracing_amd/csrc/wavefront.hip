@@ -168,14 +168,6 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x & (kSegs - 1u);
 #endif
 }
-// a claim counter's current value (a hint: the atomicAdd claims)
-__device__ __forceinline__ uint32_t ctr_peek(const uint32_t* p) {
-#ifdef RTG_HOST_EMU
-  return *p;
-#else
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
 __device__ __forceinline__ Pool pool_init() {
 #if RTG_XCD_SEGMENTS
   return Pool{0u, 0u, xcc_id(), 0u, false, false};
@@ -201,27 +193,17 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
     const int leader = __ffsll(m) - 1;
     for (;;) {
       const uint32_t lo = uint32_t((uint64_t(n) * P.seg) / segs), hi = uint32_t((uint64_t(n) * (P.seg + 1u)) / segs);
-      // the segment's claim position now (a relaxed read of its counter; the
-      // atomic below is what claims): the run is a share of what is left, so
-      // a wave that arrives late or steals from another XCD's segment takes
-      // a small run, not one sized for the whole segment (which left one wave
-      // tracing thousands of rays after the others had finished)
-      uint32_t seen = 0;
-      if (__lane_id() == leader) seen = ctr_peek(ctr + P.seg * kSegStride);
-      seen = __builtin_amdgcn_readfirstlane(__shfl(seen, leader));
-      const uint32_t from = seen < hi - lo ? lo + seen : hi;
+      const uint32_t from = P.end > lo && P.end <= hi ? P.end : lo;   // last known position in this segment
       uint32_t run = (hi - from) / (4u * wps);
       // in a segment's last 256 rays per wave a lane stops holding a
       // prefetched ray behind its current one: a ray left queued behind
       // another lane's long traversal would end the kernel that much later
       P.tail = RTG_NO_PREFETCH || (RTG_TAIL_NO_PREFETCH && run < 64u);
       run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
-      uint32_t base = hi;
-      if (from < hi) {
-        if (__lane_id() == leader) base = atomicAdd(ctr + P.seg * kSegStride, run);
-        // wave-uniform: scalar registers for the pool state
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + lo;
-      }
+      uint32_t base = 0;
+      if (__lane_id() == leader) base = atomicAdd(ctr + P.seg * kSegStride, run);
+      // wave-uniform: scalar registers for the pool state
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + lo;
       if (base < hi) {
         P.cur = base;
         P.end = hi - base > run ? base + run : hi;
@@ -527,10 +509,12 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
       uint32_t kh = asu(h.y);
       float ht = h.x;
       int hinst = int(asu(h.z));
+#ifndef RTG_DIAG_NO_VOL   // diagnostic builds only: the shading kernel without its volume tests (wrong frames)
       if (kShade == SHADE_VOL) {
         int hrefpos = int(asu(h.w));
         lifted_volumes<kCount>(sc, ro, rd, key, bounce, kh, ht, hinst, hrefpos, cnt, vrecs);
       }
+#endif
 #ifdef RTG_GUARD
       if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
 #endif
@@ -663,17 +647,22 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
                 }
               }
             }
+#ifdef RTG_DIAG_NO_VOL
+            if (false) {
+#else
             if (kShade == SHADE_VOL && flags != 0u) {
+#endif
               // a lifted volume occluding a shadow ray (camera.go:582, :639;
               // the any-hit traversal's volume test, same interval and RNG
               // domain) clears the ray: its contribution is not applied
               for (int v = 0; v < sc.num_vol_refs; ++v) {
                 float tv = 0.0f;
-                const DVolRec& R = vrecs[v];
-                if ((flags & 2u) && volume_hit_rec<kCount>(R, P, dh, 0.001f, __builtin_inff(), R.ref.ntests, key, bounce,
+                const KVolRec R = kvolrec(vrecs, v);
+                const int nt = R->ref.ntests;
+                if ((flags & 2u) && volume_hit_rec<kCount>(R, P, dh, 0.001f, __builtin_inff(), nt, key, bounce,
                                                            DOM_VOL_SH_HDRI, tv, cnt))
                   flags &= ~2u;
-                if ((flags & 1u) && volume_hit_rec<kCount>(R, P, da, 0.001f, tmax_a, R.ref.ntests, key, bounce,
+                if ((flags & 1u) && volume_hit_rec<kCount>(R, P, da, 0.001f, tmax_a, nt, key, bounce,
                                                            DOM_VOL_SH_AREA, tv, cnt))
                   flags &= ~1u;
               }
