@@ -1071,6 +1071,13 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.num_vol_refs = int32_t(h.vol_refs.size());
   d.has_volumes = h.volumes.size() > h.vol_refs.size() ? 1 : 0;
   if (d.num_vol_refs > 0) d.shade_kind = SHADE_VOL;
+  // the lean / material / volume shading variants read the tables from LDS
+  // only (flatten_scene lifts no volume when they do not fit)
+  if (h.materials.size() > size_t(kLdsMaterials) || h.textures.size() > size_t(kLdsTextures) ||
+      h.lights.size() > size_t(kLdsLights)) {
+    if (d.shade_kind == SHADE_VOL) { free_scene(ctx); return set_err(ctx, RT_ERR_INVALID, "internal: lifted volumes with tables beyond LDS"); }
+    d.shade_kind = SHADE_FULL;
+  }
   ctx->dev_nodes = ctx->dev_leaves = 0;
   ctx->build_ms = 0.0;
   if (!h.device_builds.empty() && (rc = device_builds(ctx))) { free_scene(ctx); return rc; }

@@ -321,6 +321,12 @@ struct alignas(16) DRefBox {
 enum : int32_t { SHADE_LEAN = 0, SHADE_MAT = 1, SHADE_FULL = 2, SHADE_VOL = 3 };
 
 // Everything the kernels need, passed by value as a kernel argument.
+// k_shade copies the material, texture and light tables to LDS (wavefront
+// .hip); its lean / material / volume variants read them only there, so a
+// scene with larger tables shades in the full variant (api.cpp) and keeps its
+// volumes in the world BVH (flatten_scene).
+constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
+
 struct DScene {
   const DNode4* nodes;         // BVH4 nodes, full fp32 boxes (build form; ITEM_NODE indexes it)
   const DNodeQ* qnodes;        // the same nodes quantised (RT_NODES_QUANT8; else null)

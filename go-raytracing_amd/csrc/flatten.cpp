@@ -1431,10 +1431,14 @@ int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err, c
     Flattener f(desc, out, err, opt);
     rc = f.run();
   }
-  if (rc == RT_OK && !out.vol_refs.empty() && build_vol_recs(out).empty()) {
-    // k_shade tests lifted volumes through their DVolRec records only: a
-    // volume whose boundary has none (not one leaf of <= 6 quads) stays in
-    // the world BVH, where the traversal's volume variant tests it
+  const bool big_tables = out.materials.size() > size_t(kLdsMaterials) || out.textures.size() > size_t(kLdsTextures) ||
+                          out.lights.size() > size_t(kLdsLights);
+  if (rc == RT_OK && !out.vol_refs.empty() && (big_tables || build_vol_recs(out).empty())) {
+    // k_shade tests lifted volumes through their DVolRec records only, in
+    // its volume variant, which reads the scene tables from LDS: a volume
+    // whose boundary has no record (not one leaf of <= 6 quads), or any
+    // volume of a scene whose tables do not fit in LDS, stays in the world
+    // BVH, where the traversal's volume variant tests it
     FlattenOptions o = opt;
     o.lift_volumes = 0;
     out = HostScene{};

@@ -353,7 +353,6 @@ __device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks,
 // compiled in); kShade (DScene.shade_kind): SHADE_LEAN = Lambertian /
 // DiffuseLight with solid or checker textures, SHADE_MAT = also Metal /
 // Dielectric / Isotropic, SHADE_FULL = also Noise / Image textures (and U/V).
-constexpr int kLdsMaterials = 384, kLdsTextures = 384, kLdsLights = 16;
 // The tables k_shade copies to LDS live in dynamic shared memory sized to the
 // scene (shade_lds_bytes; 0 = too large, read from global): a static
 // worst-case allocation (31.5 KB per block) capped the kernel at 5 blocks per
@@ -426,7 +425,13 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DSce
   // addresses are uniform over the wave, so these are scalar loads (a copy in
   // LDS, per-lane VGPR reads, measured C3 1496 against 1668 Msamples/s)
   const DVolRec* const vrecs = sc.vol_recs;
-  if (shade_tables_fit(sc)) {
+  // The lean / material / volume variants always read the tables from LDS
+  // (the host shades scenes whose tables do not fit with SHADE_FULL): set
+  // unconditionally, the pointers are known to be LDS pointers and every
+  // table read is a ds_read.  Chosen at run time, they were generic pointers
+  // and every material / texture / light read a flat load.
+  constexpr bool kLdsTables = kShade != SHADE_FULL;
+  if (kLdsTables || shade_tables_fit(sc)) {
     DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
     DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
     DLight* const s_light = reinterpret_cast<DLight*>(s_tex + sc.num_textures);
