@@ -404,10 +404,17 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
 #define RTG_SHADE_WAVES_FOR(kShade)                                                       \
   ((kShade) == SHADE_FULL ? RTG_SHADE_WAVES : (kShade) == SHADE_MAT ? RTG_SHADE_MAT_WAVES \
    : (kShade) == SHADE_VOL ? RTG_SHADE_VOL_WAVES : RTG_SHADE_LEAN_WAVES)
+// bounce 0's variants (camera ray generation inlined) may take their own
+// occupancy (RTG_SHADE_FIRST_WAVES > 0; A/B knob)
+#ifndef RTG_SHADE_FIRST_WAVES
+#define RTG_SHADE_FIRST_WAVES 0
+#endif
+#define RTG_SHADE_WAVES_FOR2(kShade, kFirst) \
+  ((kFirst) && RTG_SHADE_FIRST_WAVES > 0 ? RTG_SHADE_FIRST_WAVES : RTG_SHADE_WAVES_FOR(kShade))
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
 // and this kernel initialises the slot's radiance in Lout.
 template <bool kCount, bool kEnvIS, int kShade, bool kFirst>
-__global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR(kShade)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+__global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                const uint32_t* count, PathStream ns, uint32_t* ncount,
                                                uint32_t sample_base) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
@@ -1070,7 +1077,11 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     if (quant) RUN2(S, C, V, true);             \
     else RUN2(S, C, V, false);                  \
   } while (0)
-    const bool envis = sc.env.valid && sc.env.use_is, quant = sc.quant_nodes != 0;
+    // the importance-sampled HDRI is a NEE light only beside an area light
+    // (sampleLightMIS needs one, camera.go:502): without lights the kEnvIS
+    // code is dead, and its registers spilled (C5: 34 VGPRs in bounce 0's
+    // shading)
+    const bool envis = sc.env.valid && sc.env.use_is && sc.num_lights > 0, quant = sc.quant_nodes != 0;
     const int shade = sc.shade_kind;
 #if defined(RTG_RING24) && !defined(RTG_DIAG_RING)
 #define RTG_DIAG_RING 24
