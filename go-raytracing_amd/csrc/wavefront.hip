@@ -150,6 +150,11 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 #ifndef RTG_XCD_SEGMENTS
 #define RTG_XCD_SEGMENTS 1
 #endif
+// claim runs are 1/(RTG_GSS_DIV x waves per segment) of what a wave last
+// saw left in its segment
+#ifndef RTG_GSS_DIV
+#define RTG_GSS_DIV 4
+#endif
 constexpr uint32_t kSegs = 8;
 constexpr uint32_t kSegStride = 32;   // words between the segment counters
 struct Pool {
@@ -194,7 +199,12 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
     for (;;) {
       const uint32_t lo = uint32_t((uint64_t(n) * P.seg) / segs), hi = uint32_t((uint64_t(n) * (P.seg + 1u)) / segs);
       const uint32_t from = P.end > lo && P.end <= hi ? P.end : lo;   // last known position in this segment
-      uint32_t run = (hi - from) / (4u * wps);
+      // A wave that steals from another XCD's segment (its own is drained:
+      // the kernel's tail) takes the minimum run.  Sized from the segment's
+      // start, as an own-segment claim is, a late steal took up to 1/(4 wps)
+      // of a whole segment — dozens of rays per lane, traced after every
+      // other wave had finished.
+      uint32_t run = P.tried ? 0u : (hi - from) / (uint32_t(RTG_GSS_DIV) * wps);
       // in a segment's last 256 rays per wave a lane stops holding a
       // prefetched ray behind its current one: a ray left queued behind
       // another lane's long traversal would end the kernel that much later

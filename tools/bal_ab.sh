@@ -1,4 +1,8 @@
-for rep in 1 2; do for v in prev:lib_prev new:lib; do n=${v%%:*}; l=${v##*:}
+#!/bin/bash
+# Shard-balance A/B: the default bench line (no configs, PMC or CPU baseline)
+# per library variant, REPS rounds; prints value, full-frame ms and the 2/4/8-way
+# predictions, shard sums and balance.  tools/bal_ab.sh name:libdir ...
+for rep in $(seq 1 ${REPS:-2}); do for v in "$@"; do n=${v%%:*}; l=${v##*:}
 RTGPU_LIB_DIR=$l timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs --no-pmc --no-three-pass --no-count > gpurun_out/bal_${n}_$rep.json 2> gpurun_out/bal_${n}_$rep.err || exit 1
 python3 -c "
 import json; d=json.loads(open('gpurun_out/bal_${n}_$rep.json').read().strip().splitlines()[-1]); b=d['shard_balance']
