@@ -76,6 +76,14 @@ func (g *GPUBucketRenderer) initGPU(camera *Camera, world Hittable) error {
 			return err
 		}
 	}
+	// RTGPU_DEALING=dynamic: the devices claim runs of tiles as they finish
+	// (the reference's bucket channel, bucket_renderer.go:193-213) instead of
+	// the static round-robin split; for devices that differ in speed
+	if os.Getenv("RTGPU_DEALING") == "dynamic" && g.gpu.NumDevices() > 1 {
+		if err = g.gpu.SetOption(rtgpu.OptDealing, rtgpu.DealDynamic); err != nil {
+			return err
+		}
+	}
 	g.cam = GPUCameraDesc(camera)
 	g.buckets = make([]rtgpu.Bucket, len(g.BucketRenderer.buckets))
 	for i, b := range g.BucketRenderer.buckets {
