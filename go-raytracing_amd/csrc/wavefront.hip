@@ -407,7 +407,8 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
 // CornellBoxScene at 4 / 5 / 7 waves 1390 / 1454 / 1427 Msamples/s (110 / 96
 // / 72 VGPRs; 0 / 3 / 71 spilled); with the volume records (DVolRec, round
 // 4) 4 / 5 / 6 waves 1580 / 1648 / 1660 (101 / 96 / 80 VGPRs; 0 / 0 / 13
-// spilled).
+// spilled); with the records read by scalar loads, 5 / 6 / 7 waves 1886 /
+// 1927 / 1928 (96 / 80 / 72 VGPRs; 0 / 16 / 53 spilled).
 #ifndef RTG_SHADE_VOL_WAVES
 #define RTG_SHADE_VOL_WAVES 6
 #endif
