@@ -296,9 +296,11 @@ int check_render_error(rt_ctx* ctx, bool wait) {
 // for renders of more than kThreeTwinSamples samples (pixels x spp), two
 // below.  CornellBoxLucy full frame (405 M samples): one stream 1770, two
 // 1937-1952, three 1967-1970 Msamples/s; its 1/8 shards (51 M) are faster on
-// two (8-way shard prediction 7.00 vs 6.83 on three).
+// two (8-way shard prediction 6.94 / 6.99 vs 6.84 / 6.84 on three), its 1/2
+// shards (202 M) on three (2-way 1.908 / 1.917 vs 1.941 / 1.951), its 1/4
+// shards (101 M) alike (3.73 / 3.74 vs 3.75 / 3.75; round 4).
 constexpr int kDefaultTwins = 2;
-constexpr uint64_t kThreeTwinSamples = uint64_t(1) << 28;
+constexpr uint64_t kThreeTwinSamples = uint64_t(1) << 26;
 
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
