@@ -270,6 +270,25 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, vals) -> list:
+        """Every rank's list of floats, on every rank (N > 1 diagnostics)."""
+        if self.dist is None:
+            return [list(vals)]
+        import torch
+        dev = self.dev if self.backend == "nccl" else "cpu"
+        t = torch.tensor(list(vals), dtype=torch.float64, device=dev)
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [[float(x) for x in o.cpu().tolist()] for o in out]
+
+    def sum_int(self, x: int) -> int:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.int64, device=self.dev if self.backend == "nccl" else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return int(t.item())
+
     def reduce_frame(self, accum):
         if self.dist is None:
             return
@@ -308,6 +327,7 @@ def dynamic_runs(add, ntiles: int, world: int, first_pct: int = 50):
 
 class Workload:
     """One scene resident on this rank's GPU, this rank's bucket shard."""
+    _instances = 0   # per process: makes the dynamic-dealing store keys unique per workload
 
     def __init__(self, g, D: Dist, scene: str, scene_kw: dict, seed: int, blas: str, nodes: str = "fp32",
                  devices=None, dealing: str = "static"):
@@ -340,8 +360,16 @@ class Workload:
         if devices is not None:
             self.ctx.set_dealing(dealing)
         self.all_tiles = g.split_buckets(self.buckets, SHARD_TILE)
+        # static dealing: this rank's share of the tiles
+        self.my_tiles = len(g.shard_buckets(self.buckets, D.rank, D.world, SHARD_TILE))
+        # the store counters of dynamic dealing live as long as the process
+        # group: every workload (the main one, each config scene) and every
+        # frame needs keys of its own, or a later workload finds them drained
+        Workload._instances += 1
+        self.uid = f"{scene}_{self.W}x{self.H}_{Workload._instances}"
         self.frame_no = 0
-        self.tiles_rendered = 0
+        self.tiles_rendered = self.my_tiles
+        self.reduce_ms = []
         self.accum = torch.zeros(self.H * self.W * 3, dtype=torch.float32, device=D.dev)
         self.stream = torch.cuda.current_stream(D.dev)
         self.kernel_ms, self.kernel_times = [], []
@@ -350,7 +378,7 @@ class Workload:
         self.accum.zero_()
         if self.dealing == "dynamic" and self.D.world > 1:
             store = self.D.store()
-            key = f"rtgpu_deal_{self.frame_no}"
+            key = f"rtgpu_deal_{self.uid}_{self.frame_no}"
             self.frame_no += 1
             self.tiles_rendered = 0
             for a, b in dynamic_runs(lambda k: store.add(key, k), len(self.all_tiles), self.D.world):
@@ -365,7 +393,36 @@ class Workload:
             self.kernel_ms.append(self.ctx.last_render_kernel_ms())
             if kernel_timing:
                 self.kernel_times.append(self.ctx.last_kernel_times())
-        self.D.reduce_frame(self.accum)
+        if timed and self.D.world > 1:
+            # the combine on its own: CUDA events on the render stream (RCCL
+            # runs on torch's current stream), a host clock for gloo
+            import torch
+            if self.D.backend == "nccl":
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
+                self.D.reduce_frame(self.accum)
+                e1.record(self.stream)
+                self.reduce_ms.append((e0, e1))
+            else:
+                t0 = time.perf_counter()
+                self.D.reduce_frame(self.accum)
+                self.reduce_ms.append((time.perf_counter() - t0) * 1e3)
+        else:
+            self.D.reduce_frame(self.accum)
+
+    def reduce_ms_avg(self):
+        """Mean ms of the timed steps' frame combine (events: after the sync)."""
+        v = [x[0].elapsed_time(x[1]) if isinstance(x, tuple) else x for x in self.reduce_ms]
+        return float(sum(v) / len(v)) if v else 0.0
+
+    def check_dealing(self):
+        """Dynamic dealing: the ranks' tiles of the last frame must partition
+        the tile list (an empty or partial frame must never be reported as a
+        throughput)."""
+        if self.dealing == "dynamic" and self.D.world > 1:
+            total = self.D.sum_int(self.tiles_rendered)
+            if total != len(self.all_tiles):
+                raise RuntimeError(f"dynamic dealing rendered {total} of {len(self.all_tiles)} tiles")
 
     def run(self, steps: int, warmup: int, kernel_timing: bool = False) -> float:
         """Barrier + synchronize on both sides of exactly `steps` timed steps;
@@ -382,7 +439,9 @@ class Workload:
             self.step(True, kernel_timing)
         torch.cuda.synchronize(self.D.dev)
         self.D.barrier()
-        return self.D.max(time.perf_counter() - t0)
+        el = self.D.max(time.perf_counter() - t0)
+        self.check_dealing()
+        return el
 
     def frame_sum(self):
         # identical for any rank count: each pixel has one contributor and the
@@ -510,6 +569,30 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     img_ok = bool(__import__("torch").isfinite(w.accum).all().item()) if D.rank == 0 else True
     frame_sum = w.frame_sum()
+    # N > 1: what the driver's scaling line cannot show by itself — each
+    # rank's render time and tile count and the combine's own time, so a
+    # 1->N curve splits into imbalance, per-render fixed cost and reduce
+    rank_diag = None
+    if D.world > 1:
+        rows = D.gather([float(np.mean(w.kernel_ms)) if w.kernel_ms else 0.0, w.reduce_ms_avg(),
+                         float(w.tiles_rendered)])
+        rank_diag = {"render_ms": [round(r[0], 3) for r in rows], "reduce_ms": [round(r[1], 3) for r in rows],
+                     "tiles": [int(r[2]) for r in rows], "tiles_total": len(w.all_tiles),
+                     "note": "per rank, mean over the timed steps: render = device time of the render's kernels "
+                             "(rt_last_render_kernel_ms), reduce = the frame combine to rank 0 (events on the "
+                             "render stream for RCCL), tiles = 16x16 tiles rendered in the last step"}
+    # The timed region ends with the frame in HBM (the C-ABI's device-buffer
+    # entry point).  rt_render into host buffers adds one D2H copy of the
+    # float3 frame: timed here once, after the timed steps, and reported beside
+    # `value` (never as it).
+    d2h_ms = None
+    if D.rank == 0:
+        import torch
+        torch.cuda.synchronize(D.dev)
+        t_d = time.perf_counter()
+        _host = w.accum.cpu()
+        d2h_ms = (time.perf_counter() - t_d) * 1e3
+        del _host
 
     roofline = None
     kernels = None
@@ -686,7 +769,17 @@ def main():
                        "image_finite": img_ok, "frame_sum": frame_sum},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "timed_region": {
+                "inside": "every sample of the frame rendered (all bounces, all kernels) into a device float3 "
+                          "accumulation buffer" + ("; the RCCL reduce of the frame to rank 0" if D.world > 1 else ""),
+                "outside": "scene flatten / upload (resident before the clock starts); the D2H copy of the frame "
+                           "that rt_render into host buffers adds (d2h_ms, measured once after the timed steps)",
+                "d2h_ms": round(d2h_ms, 3) if d2h_ms is not None else None,
+                "value_with_d2h": round(w.samples() / ((ms_per_step + d2h_ms) / 1e3) / 1e6, 3)
+                if d2h_ms is not None else None},
         }
+        if rank_diag is not None:
+            line["ranks"] = rank_diag
         if args.dealing == "dynamic":
             if devices is not None:
                 tiles, runs = w.ctx.last_dealing()

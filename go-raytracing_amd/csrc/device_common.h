@@ -23,10 +23,11 @@ namespace rtg {
 // RTG_GUARD (diagnostic build only, never the product): every device array
 // index is checked against its length; a bad index is clamped and counted,
 // and the first one's site / index / length are kept in rtg_guard_rec for
-// the host (rtg_guard_report after each render).  No device printf: its
-// hostcall requests aborted the runtime ("Hostcall: invalid service request")
-// inside these persistent kernels, which is what made round 2's guard builds
-// fault and drift.
+// the host (rtg_guard_report after each render).  No device printf.  (Round
+// 2-3's guard builds faulted and aborted with "Hostcall: invalid service
+// request": the cause was an out-of-bounds store past the queue buffer with
+// 3-4 twin streams, found by the round-4 canaries and fixed in api.cpp —
+// DESIGN.md §7.)
 #ifdef RTG_GUARD
 __device__ unsigned int rtg_guard_rec[4];   // count, site, index, length of the first bad index
 __device__ __forceinline__ void rtg_guard_note(int site, uint32_t i, uint32_t n) {

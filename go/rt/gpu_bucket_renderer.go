@@ -17,6 +17,7 @@ package rt
 
 import (
 	"fmt"
+	"log"
 	"os"
 	"time"
 
@@ -69,6 +70,9 @@ func (g *GPUBucketRenderer) initGPU(camera *Camera, world Hittable) error {
 		}
 	}
 	if g.gpu == nil {
+		// say why the other devices are not used: an out-of-memory or
+		// peer-access failure would otherwise only show up as lower speed
+		log.Printf("rt: GPU renderer on all devices failed (%v); using device 0 only", err)
 		if g.gpu, err = rtgpu.New(0); err != nil {
 			return err
 		}

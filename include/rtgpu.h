@@ -40,7 +40,12 @@ enum rt_status {
   RT_OK = 0,
   RT_ERR_INVALID = -1,     /* bad argument / malformed scene graph          */
   RT_ERR_UNSUPPORTED = -2, /* Go type or nesting the GPU path does not take;
-                              the caller falls back to rt.BucketRenderer     */
+                              the caller falls back to rt.BucketRenderer.
+                              Includes a BVH whose worst traversal needs more
+                              than 64 stack entries; a scene holding a
+                              RotateX / RotateZ wrapper traverses in the
+                              reference's DFS order with two words per entry
+                              (DESIGN.md §3), so its limit is 32 entries    */
   RT_ERR_HIP = -3,         /* HIP runtime error (message in rt_last_error)  */
   RT_ERR_OOM = -4,         /* device allocation failed                      */
   RT_ERR_NO_SCENE = -5,    /* rt_render before rt_scene_upload              */
@@ -322,7 +327,10 @@ int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t ma
  *   RT_OPT_STREAMS: 1..4: the bucket tiles are dealt to that many parts
  *     ("twins"), each rendered on its own HIP stream, so one part's kernel
  *     tails overlap the others' kernels; 1 keeps one stream.  Default: 3
- *     for renders of more than 2^28 samples (pixels x spp), else 2.
+ *     for renders of more than 2^26 samples (pixels x spp), else 2; scenes
+ *     whose shading tests lifted volumes (RT_VOLUMES_LIFTED with a Volume
+ *     in the scene) always render on 1 (the shading kernel is the long one
+ *     there, and more parts only add launch overlap it cannot use).
  *   RT_OPT_DEALING (multi-device contexts): how a render deals its 16x16
  *     tiles to the devices.  RT_DEAL_STATIC (default) = tile k to device
  *     k mod n, every share rendered at once, asynchronously.

@@ -7,7 +7,9 @@ the GPU and gloo carrying the reduce (RTGPU_BENCH_BACKEND=gloo): bucket
 sharding, the per-rank renders, the combine to rank 0, the barrier/max-over-
 ranks timing and the JSON line are the production code.  The combined
 frame's checksum must equal the single-rank run's exactly (every pixel has
-one contributor; the RNG is keyed by global pixel id)."""
+one contributor; the RNG is keyed by global pixel id).  The line must also
+split the multi-rank step into each rank's render time and tile count and
+the combine's own time (`ranks`), and state its timed region."""
 import json
 import os
 import socket
@@ -48,3 +50,11 @@ def test_two_ranks_combine_to_the_single_rank_frame(dealing):
     assert b["config"]["parallelism"] == ("tiles-rr2" if dealing == "static" else "tiles-dyn2")
     assert a["config"]["image_finite"] and b["config"]["image_finite"]
     assert a["config"]["frame_sum"] == b["config"]["frame_sum"] > 0
+    # a scaling line splits into per-rank render time, tiles and the combine
+    r = b["ranks"]
+    assert len(r["render_ms"]) == len(r["reduce_ms"]) == len(r["tiles"]) == 2
+    assert sum(r["tiles"]) == r["tiles_total"] and min(r["tiles"]) > 0
+    assert all(x > 0 for x in r["render_ms"]) and all(x >= 0 for x in r["reduce_ms"])
+    assert "ranks" not in a
+    for line in (a, b):
+        assert line["timed_region"]["d2h_ms"] > 0 and line["timed_region"]["value_with_d2h"] < line["value"]

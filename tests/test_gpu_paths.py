@@ -12,9 +12,16 @@ sampleAreaLight's :639).
 For every path whose incoming ray is bit-identical on both sides, the hit ids
 and t must be equal, and so must the NEE rays traced and their visibility
 (a lifted volume occluding a shadow ray is resolved in shading: the GPU then
-has no such ray, the oracle an occluded one).  Paths whose rays differ
-("diverged": an earlier bounce rounded differently) are counted and reported
-and bounded, never compared.
+has no such ray, the oracle an occluded one; the volume scenes therefore also
+run with RT_VOLUMES_IN_BVH, where every shadow ray is traced and the traced
+flags must match exactly).  Paths whose rays differ ("diverged": an earlier
+bounce rounded differently) are counted and reported and bounded, never
+compared.
+
+Depth: every bounce the reference recurses through, up to the scene's
+MaxDepth (camera.go:443-518) — RandomScene's 50 (scenes.go:72-73) and
+HDRITestScene's 20 (scenes.go:444-445) — or until no path is alive on either
+side.
 """
 import numpy as np
 import pytest
@@ -22,15 +29,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 SEED = 29
-BOUNCES = 5
-# (scene, constructor kwargs, samples probed, max share of diverged paths)
+LIFTED, IN_BVH = 0, 1
+# (id, scene, constructor kwargs, samples probed, max share of diverged
+# paths, bounces probed (0: the scene's MaxDepth), volume placement)
 CASES = [
-    ("cornell-lucy", dict(width=320, aspect=16.0 / 9.0), (0, 5), 2e-3),   # C4, full 280K mesh
-    ("cornell", dict(width=128), (0, 5), 2e-3),                           # C3, fog + area light
-    ("random", dict(width=192), (0, 5), 2e-3),                            # C2, spheres, metal, glass
-    ("cornell-smoke", dict(width=96), (0,), 2e-3),                        # two lifted volumes
-    ("cornell-rotations", dict(width=96), (0,), 2e-3),                    # RotateX/Z, Scale chains
-    ("hdri-nee", dict(width=96), (0,), 2e-2),                             # HDRI importance sampling + area light
+    ("cornell-lucy", "cornell-lucy", dict(width=320, aspect=16.0 / 9.0), (0, 5), 2e-3, 0, LIFTED),  # C4, 280K mesh
+    ("cornell", "cornell", dict(width=128), (0, 5), 2e-3, 0, LIFTED),              # C3, fog + area light
+    ("cornell-in-bvh", "cornell", dict(width=96), (0,), 2e-3, 0, IN_BVH),          # C3, fog traversed in the BVH
+    ("random", "random", dict(width=192), (0, 5), 2e-3, 0, LIFTED),                # C2 to MaxDepth 50
+    ("hdri-test", "hdri-test", dict(width=192), (0, 3), 2e-2, 0, LIFTED),          # C5 to MaxDepth 20
+    ("cornell-smoke", "cornell-smoke", dict(width=96), (0,), 2e-3, 0, LIFTED),     # two lifted volumes
+    ("cornell-smoke-in-bvh", "cornell-smoke", dict(width=96), (0,), 2e-3, 0, IN_BVH),
+    ("cornell-rotations", "cornell-rotations", dict(width=96), (0,), 2e-3, 0, LIFTED),  # RotateX/Z, Scale chains
+    ("hdri-nee", "hdri-nee", dict(width=96), (0,), 2e-2, 0, LIFTED),               # HDRI IS + area light
 ]
 
 
@@ -38,19 +49,27 @@ def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def compare_paths(g, O, name, kw, samples):
+def compare_paths(g, O, name, kw, samples, bounces=0, volumes=LIFTED):
     """Per bounce and sample: (alive paths, compared, diverged, id/t mismatches,
     NEE mismatches).  Raises nothing; the caller asserts."""
     s = g.Scene(name, **kw)
     cam = s.camera
+    nb = bounces or cam.max_depth
     c = g.Context(0)
     rows = []
     try:
+        c.set_option(g.RT_OPT_VOLUMES, g.RT_VOLUMES_IN_BVH if volumes == IN_BVH else g.RT_VOLUMES_LIFTED)
         c.upload(s.desc)
         lifted = c.info().volumes > 0
         for sample in samples:
-            ot, op, ott, oray, onee = O.path_records(s.desc, cam, SEED, sample, BOUNCES, fp32=True, threads=16)
-            for b in range(BOUNCES):
+            ot, op, ott, oray, onee = O.path_records(s.desc, cam, SEED, sample, nb, fp32=True, threads=16)
+            for b in range(nb):
+                if not np.any(ot[b] != -2):   # no path left on the oracle's side: the GPU must agree
+                    gt = c.extend_hits(cam, SEED, sample, b)[0]
+                    rows.append(dict(sample=sample, bounce=b, alive=int(np.sum(gt != -2)), compared=0,
+                                     diverged=int(np.sum(gt != -2)), hit_mismatch=0, nee_mismatch=0, shadow_rays=0,
+                                     first_bad=[]))
+                    break
                 gt, gp, gtt, gray = c.extend_hits(cam, SEED, sample, b)
                 gnee = c.shadow_visibility(cam, SEED, sample, b)
                 alive_g, alive_o = gt != -2, ot[b] != -2
@@ -76,14 +95,17 @@ def compare_paths(g, O, name, kw, samples):
     return rows
 
 
-@pytest.mark.parametrize("name,kw,samples,max_div", CASES, ids=[c[0] for c in CASES])
-def test_bounce_hits_and_shadow_rays_bit_exact(g, O, name, kw, samples, max_div):
-    rows = compare_paths(g, O, name, kw, samples)
+@pytest.mark.parametrize("cid,name,kw,samples,max_div,bounces,volumes", CASES, ids=[c[0] for c in CASES])
+def test_bounce_hits_and_shadow_rays_bit_exact(g, O, cid, name, kw, samples, max_div, bounces, volumes):
+    rows = compare_paths(g, O, name, kw, samples, bounces, volumes)
     for r in rows:
-        print(f"{name} sample {r['sample']} bounce {r['bounce']}: alive {r['alive']} compared {r['compared']} "
+        print(f"{cid} sample {r['sample']} bounce {r['bounce']}: alive {r['alive']} compared {r['compared']} "
               f"diverged {r['diverged']} shadow rays {r['shadow_rays']} hit mismatches {r['hit_mismatch']} "
               f"NEE mismatches {r['nee_mismatch']}")
     assert sum(r["compared"] for r in rows if r["bounce"] > 0) > 0
+    deepest = max(r["bounce"] for r in rows if r["compared"] > 0)
+    print(f"{cid}: deepest compared bounce {deepest}, paths compared {sum(r['compared'] for r in rows)}, "
+          f"diverged {sum(r['diverged'] for r in rows)}")
     for r in rows:
         assert r["hit_mismatch"] == 0 and r["nee_mismatch"] == 0, f"{name}: {r}"
         assert r["diverged"] <= max_div * max(r["alive"], 1), f"{name}: too many diverged paths {r}"
