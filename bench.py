@@ -44,7 +44,8 @@ sys.path.insert(0, ROOT)
 
 # Algorithmic bytes per unit of work.
 BYTES = {
-    "node_visits": 128,      # one BVH4 node (DNode4): four 24-B child boxes + four child items (64 B with --nodes quant8)
+    "node_visits": 128,      # one BVH4 node (DNode4): four 24-B child boxes + four child items; set from the
+                             # format the kernels run: 64 (quant8 DNodeQ), 80 (wide8: the five 16-B loads of a DNode8)
     "tri_tests": 36,         # v0, e1, e2 fp32
     "sphere_tests": 32,
     "quad_tests": 64,
@@ -90,8 +91,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=0, help="0: scene default")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--nodes", choices=["fp32", "quant8"], default="fp32",
-                    help="BVH4 node format (RT_OPT_NODE_FORMAT)")
+    ap.add_argument("--nodes", choices=["fp32", "quant8", "wide8"], default="fp32",
+                    help="node format (RT_OPT_NODE_FORMAT): BVH4 fp32 / quantised, or 8-wide quantised")
     ap.add_argument("--blas", choices=["sah", "reference", "device"], default="sah",
                     help="mesh BLAS builder: host SAH (default), the caller's topology, or the GPU LBVH "
                          "(build.hip); the world BVH is SAH except for 'reference'")
@@ -551,8 +552,6 @@ def main():
         scene_kw["spp"] = args.spp
     if args.depth:
         scene_kw["max_depth"] = args.depth
-    if args.nodes == "quant8":
-        BYTES["node_visits"] = 64   # one DNodeQ
     # --gpus N without torchrun: one process, one multi-device context over
     # devices 0..N-1 (RTGPU_BENCH_DEVICES=0,0 repeats a device on a one-GPU box)
     devices = None
@@ -561,6 +560,10 @@ def main():
         devices = [int(x) for x in env_dev.split(",")] if env_dev else list(range(args.gpus))
     w = Workload(g, D, args.scene, scene_kw, args.seed, args.blas, args.nodes, devices, args.dealing)
     W, H, spp, depth = w.W, w.H, w.spp, w.depth
+    # bytes a node step reads in the format the kernels run (a scene that
+    # does not take the format asked for keeps fp32 BVH4 nodes)
+    node_format = {g.RT_NODES_FP32: "fp32", g.RT_NODES_QUANT8: "quant8", g.RT_NODES_WIDE8: "wide8"}[w.info.node_format]
+    BYTES["node_visits"] = {"fp32": 128, "quant8": 64, "wide8": 80}[node_format]
 
     # one HIP event before each extend/shade/shadow launch (and after each
     # shadow launch) on the render stream: per-kernel launch durations
@@ -763,8 +766,8 @@ def main():
             "config": {"workload": f"{args.scene} {W}x{H} {spp}spp depth {depth}", "scene": args.scene,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "parallelism": (f"tiles-{'rr' if args.dealing == 'static' else 'dyn'}{D.world}" if devices is None
-                                       else f"ctx-multi{devices}-{args.dealing}"), "buckets": len(w.buckets), "blas": args.blas, "nodes": args.nodes,
-                       "triangles": w.info.triangles, "bvh_nodes": w.info.nodes,
+                                       else f"ctx-multi{devices}-{args.dealing}"), "buckets": len(w.buckets), "blas": args.blas, "nodes": node_format,
+                       "triangles": w.info.triangles, "bvh_nodes": w.info.nodes, "bvh_nodes8": w.info.nodes8,
                        "scene_build_s": round(w.build_s, 2), "device_bvh_build_ms": round(w.dev_build_ms, 2),
                        "image_finite": img_ok, "frame_sum": frame_sum},
             "roofline": roofline,

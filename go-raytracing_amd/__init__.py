@@ -35,7 +35,7 @@ RT_VOLUMES_LIFTED, RT_VOLUMES_IN_BVH = 0, 1
 RT_OPT_BVH4_COLLAPSE = 9
 RT_COLLAPSE_SAH, RT_COLLAPSE_GREEDY = 0, 1
 RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
-RT_NODES_FP32, RT_NODES_QUANT8 = 0, 1
+RT_NODES_FP32, RT_NODES_QUANT8, RT_NODES_WIDE8 = 0, 1, 2
 RT_OPT_DEALING, RT_OPT_DEAL_FIRST = 10, 11
 RT_DEAL_STATIC, RT_DEAL_DYNAMIC = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
@@ -132,7 +132,8 @@ class RtKernelTimes(C.Structure):
 class RtSceneInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("nodes", "leaves", "refs", "spheres", "quads", "triangles", "planes",
                                          "instances", "blases", "volumes", "materials", "textures", "lights",
-                                         "stack_needed", "tlas_depth", "blas_depth")] + [("device_bytes", C.c_int64)]
+                                         "stack_needed", "tlas_depth", "blas_depth")] + [("device_bytes", C.c_int64)] + \
+        [("node_format", C.c_int32), ("nodes8", C.c_int32)]
 
 
 class RtsSceneOptions(C.Structure):
@@ -528,7 +529,7 @@ class Context:
     def set_node_format(self, fmt: str):
         """BVH4 node records: "fp32" (default, 128 B) or "quant8" (64 B,
         8-bit child planes with a conservative margin); next upload."""
-        self.set_option(RT_OPT_NODE_FORMAT, {"fp32": RT_NODES_FP32, "quant8": RT_NODES_QUANT8}[fmt])
+        self.set_option(RT_OPT_NODE_FORMAT, {"fp32": RT_NODES_FP32, "quant8": RT_NODES_QUANT8, "wide8": RT_NODES_WIDE8}[fmt])
 
     def set_collapse(self, collapse: str):
         """BVH2 -> BVH4 collapse: "sah" (default, least total node area) or

@@ -882,8 +882,9 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
     return RT_OK;
   }
   if (key == RT_OPT_NODE_FORMAT) {
-    if (value != RT_NODES_FP32 && value != RT_NODES_QUANT8) return set_err(ctx, RT_ERR_INVALID, "bad node format");
-    ctx->fopt.quant_nodes = value == RT_NODES_QUANT8 ? 1 : 0;
+    if (value != RT_NODES_FP32 && value != RT_NODES_QUANT8 && value != RT_NODES_WIDE8)
+      return set_err(ctx, RT_ERR_INVALID, "bad node format");
+    ctx->fopt.quant_nodes = value == RT_NODES_QUANT8 ? 1 : value == RT_NODES_WIDE8 ? 2 : 0;
     return RT_OK;
   }
   if (key == RT_OPT_VOLUMES) {
@@ -972,7 +973,7 @@ static int device_builds(rt_ctx* ctx) {
                           ctx->stream));
   }
   h.stack_needed = (h.tlas_need4 + h.max_leaf_inst + 1 + need + 2) * (h.dfs_order ? 2 : 1);
-  if (h.stack_needed > kStackMax)
+  if (h.stack_needed > 64)   // the BVH4 bound (the probe kernels' LDS stack)
     return set_err(ctx, RT_ERR_UNSUPPORTED, "device-built BVH too deep for the traversal stack");
   d.stack_needed = h.stack_needed;
   d.n_nodes = tgt.nodes_used;
@@ -1040,6 +1041,11 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(env_pdf, env.pdf);
   UP(env_marginal, env.marginal);
   UP(env_conditional, env.conditional);
+  if (h.wide_nodes) {
+    UP(nodes8, nodes8);
+    UP(litems, litems);
+    UP(wtris, wtris);
+  }
 #undef UP
   d.tlas = h.tlas;
   d.env.valid = h.env_valid;
@@ -1055,11 +1061,15 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   d.stack_needed = h.stack_needed;
   d.quant_nodes = h.quant_nodes;
   d.dfs_order = h.dfs_order;
+  d.wide_nodes = h.wide_nodes;
+  d.root8 = h.root8;
+  if (h.wide_nodes) d.stack_needed = std::max(h.stack_needed, h.stack_needed8);
   d.n_nodes = uint32_t(h.nodes4.size()); d.n_leaves = uint32_t(h.leaves.size()); d.n_refs = uint32_t(h.refs.size());
   d.n_spheres = uint32_t(h.spheres.size()); d.n_quads = uint32_t(h.quads.size()); d.n_tris = uint32_t(h.tris.size());
   d.n_instances = uint32_t(h.instances.size()); d.n_blas = uint32_t(h.blas.size());
   d.n_volumes = uint32_t(h.volumes.size());
   d.n_circles = uint32_t(h.circles.size());
+  d.n_nodes8 = uint32_t(h.nodes8.size()); d.n_litems = uint32_t(h.litems.size()); d.n_wtris = uint32_t(h.wtris.size());
   d.shade_kind = SHADE_LEAN;   // the k_shade variant (wavefront.hip)
   for (const DMaterial& m : h.materials)
     if (m.kind == RT_METAL || m.kind == RT_DIELECTRIC || m.kind == RT_ISOTROPIC) d.shade_kind = SHADE_MAT;
@@ -1145,6 +1155,8 @@ int rt_scene_get_info(const rt_ctx* ctx, rt_scene_info* o) {
   o->tlas_depth = h.tlas_depth;
   o->blas_depth = h.blas_depth;
   o->device_bytes = int64_t(ctx->scene_bytes);
+  o->node_format = h.wide_nodes ? RT_NODES_WIDE8 : h.quant_nodes ? RT_NODES_QUANT8 : RT_NODES_FP32;
+  o->nodes8 = int(h.nodes8.size());
   return RT_OK;
 }
 

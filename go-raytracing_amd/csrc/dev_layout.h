@@ -37,6 +37,10 @@ enum : uint32_t {
   ITEM_WSPHERE = 9u,    // a world sphere: index = sphere index
   ITEM_WINST = 10u,     // a world instance: index = ref position; its culling
                         // box and entry record are one DInstEntry
+  // 8-wide node format (RT_NODES_WIDE8, DNode8) only:
+  ITEM_LREF = 11u,      // a leaf child whose item is litems[index] (world leaves)
+  ITEM_WTRI1 = 12u,     // tags 12..13: a triangle leaf of (tag - 11) DWTri records
+                        // at wtris[index..] (mesh BLAS leaves, one gather)
 };
 constexpr int ITEM_SHIFT = 28;
 constexpr uint32_t ITEM_MASK = (1u << ITEM_SHIFT) - 1u;
@@ -51,9 +55,10 @@ __host__ __device__ inline bool item_is_tri_leaf(uint32_t tag) {
 // Leaf-like items (tested in place; the lane carries on with its stack):
 // a DLeaf record, an inline triangle leaf, an inline world quad / sphere.
 // (Instance items are not: they switch the lane's ray.)
+__host__ __device__ inline bool item_is_wtri_leaf(uint32_t tag) { return tag == ITEM_WTRI1 || tag == ITEM_WTRI1 + 1u; }
 __host__ __device__ inline bool item_is_leaf(uint32_t item) {
   const uint32_t tag = item >> ITEM_SHIFT;
-  return tag == ITEM_LEAF || item_is_tri_leaf(tag) || tag == ITEM_WQUAD || tag == ITEM_WSPHERE;
+  return tag == ITEM_LEAF || item_is_tri_leaf(tag) || tag == ITEM_WQUAD || tag == ITEM_WSPHERE || item_is_wtri_leaf(tag);
 }
 
 // Primitive reference kinds (leaf "kind" field and ref tags).
@@ -121,6 +126,55 @@ struct alignas(64) DNodeQ {
   uint32_t item[4];  // child items, as DNode4
 };
 static_assert(sizeof(DNodeQ) == 64, "DNodeQ: half an L2 line");
+
+// 8-wide quantised node, 128 B (one L2 line; RT_NODES_WIDE8).  Collapsed
+// from the same SAH BVH2 as DNode4 with the SAH-optimal cut generalised to
+// eight children (flatten.cpp build_bvh8).  What a node step reads is five
+// 16-B loads for eight children (DNode4: seven for four):
+//   [0,16)  org.xyz (per-axis frame origin), child_base
+//   [16,32) leaf_base, step.x | step.y (bf16, high | low half), step.z (bf16,
+//           high half) | imask << 8 | lmask, twomask | flags << 8
+//   [32,56) X planes: lo[8] hi[8] lo[8] (one byte per child slot); the
+//           traversal loads 16 B at +0 (lo, hi) or +8 (hi, lo) by the sign of
+//           the ray direction, so the near / far rows arrive in order
+//   [56,80) Y planes, [80,104) Z planes; [104,128) unused.
+// A plane q steps from the origin is at t = fma(q, inv * step, (org - o) *
+// inv), the RT_NODES_QUANT8 form; every child box holds its fp32 BVH2 box
+// widened by the quantiser's margin (node_quant.h), so box tests stay
+// conservative and hits are unchanged.  Child slots are ordered by octant
+// (slot bit k = the child lies on the + side of the node centre on axis k);
+// a ray whose direction signs form octant o visits slot o ^ j for j = 0..7,
+// roughly near to far, with no sort.
+//   imask: slots holding internal nodes: node index child_base + (rank of the
+//          slot among them)
+//   lmask: slots holding leaves (an unused slot has lo = 255, hi = 0 on every
+//          axis and is never hit)
+//   flags & 1 (tri node): every leaf is a triangle leaf of 1 or 2 triangles:
+//          ITEM_WTRI1/2 at wtris[leaf_base + (triangles of the leaf slots
+//          below it)], twomask = the 2-triangle leaves; else every leaf's
+//          item is litems[leaf_base + (rank among the leaf slots)]
+struct alignas(128) DNode8 {
+  float org[3];
+  uint32_t child_base;
+  uint32_t leaf_base;
+  uint32_t sxy;
+  uint32_t sz_masks;
+  uint32_t meta;
+  uint32_t q[18];     // X: lo(2 words) hi(2) lo(2); Y; Z
+  uint32_t pad[6];
+};
+static_assert(sizeof(DNode8) == 128, "DNode8: one L2 line");
+constexpr uint32_t kNode8Tri = 1u;   // DNode8.meta flags (bits 8..15)
+
+// A triangle of an 8-wide tri node's leaf, 40 B: the traversal record (v0,
+// e1, e2, as DTri) and the triangle's index in the scene's triangle arrays
+// (hit records, ranks and shading read that one).  The leaves' triangles
+// are copied in leaf order, so a 2-triangle leaf is one 80-B gather.
+struct DWTri {
+  float v0[3], e1[3], e2[3];
+  int32_t tri;
+};
+static_assert(sizeof(DWTri) == 40, "DWTri: 40 B");
 
 struct alignas(8) DLeaf {
   uint32_t first;  // index into refs (PK_MIXED) or into the kind's prim array
@@ -214,7 +268,8 @@ struct alignas(128) DInstEntry {
   float chi[3]; int32_t nwrap;       // culling box hi
   float p0[3]; uint32_t root_item;   // wrapper 0 ray-side floats: translate: offset; rotate: sin, cos, -;
   float p1[3]; int32_t check_box;    //   scale: 1/factor;  BLAS root item, root-box test flag
-  float rlo[3]; int32_t pad1;        // BLAS root box (object space)
+  float rlo[3]; uint32_t root8;      // BLAS root box (object space); the BLAS root item in the
+                                     // 8-wide node format (RT_NODES_WIDE8)
   float rhi[3]; int32_t pad2;
   float p2[3]; int32_t pad0;         // (the traversal gathers the first 112 B: wrappers 0-2 + root box)
   float p3[3]; int32_t pad3;
@@ -381,8 +436,16 @@ struct DScene {
   int32_t needs_uv;       // an ImageTexture exists: hit records carry U/V
   int32_t quant_nodes;    // traverse the quantised DNodeQ nodes (RT_NODES_QUANT8), else DNode4
   int32_t dfs_order;      // closest hit in the reference's DFS order with exact box culls (RotateX/Z scenes; trav_step)
+  // 8-wide node format (RT_NODES_WIDE8): the traversal kernels without the
+  // rare-primitive variant read these instead of `nodes`
+  int32_t wide_nodes;
+  uint32_t root8;              // the world BVH's root item in that format
+  const DNode8* nodes8;
+  const uint32_t* litems;      // leaf items of the non-triangle nodes
+  const DWTri* wtris;          // the tri nodes' triangles in leaf order
   // array lengths (bounds checks of the RTG_GUARD diagnostic build)
   uint32_t n_nodes, n_leaves, n_refs, n_spheres, n_quads, n_tris, n_instances, n_blas, n_volumes, n_circles;
+  uint32_t n_nodes8, n_litems, n_wtris;
 };
 
 struct DCamera {

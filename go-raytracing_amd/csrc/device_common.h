@@ -818,6 +818,14 @@ constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackV
 #define RTG_P2_SLACK 0
 #endif
 constexpr int kP2Slack = RTG_P2_SLACK;
+// BVH4 fp32 slab arithmetic in packed fp32 (v_pk_add_f32 / v_pk_mul_f32):
+// half the slab VALU instructions, bit-identical, but measured slower (C4
+// 2018 -> 1934 Msamples/s, k_extend 99.5 -> 107 ms per frame: 13 VGPRs
+// spilled at the 72-register cap and the packed ops issue no faster than
+// two scalar ones, MI355X_MICROARCH.md); kept as a diagnostic variant
+#ifndef RTG_PK_SLAB
+#define RTG_PK_SLAB 0
+#endif
 
 // Schedule independence of the closest hit (DESIGN §3 "Determinism").  The
 // result must not depend on which rays share a wave or on when a wave runs:
@@ -882,7 +890,7 @@ __device__ __forceinline__ Best trav_best(const Trav& T, const TStack& S) {
 }
 
 // Set up one ray: planes (lifted out of the BVH) and the root box.
-template <bool kAny, bool kCount>
+template <bool kAny, bool kCount, bool kWide = false>
 __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack& S, V3 wo, V3 wd, float time,
                                          float tmin, float tmax, uint32_t key, uint32_t bounce, uint32_t voldom,
                                          Cnt& cnt) {
@@ -907,7 +915,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
       !box_hit(sc.tlas.box[0], sc.tlas.box[1], sc.tlas.box[2], sc.tlas.box[3], sc.tlas.box[4], sc.tlas.box[5],
                T.cr, tmin, kAny ? tmax : T.bt, tn))
     return TRAV_DONE;
-  T.item = sc.tlas.root_item;
+  T.item = kWide ? sc.root8 : sc.tlas.root_item;
   if ((T.item >> ITEM_SHIFT) != ITEM_NODE) {
     T.lf = T.item;
     T.item = item_is_leaf(T.lf) ? ITEM_NONE : ITEM_POP;
@@ -922,7 +930,7 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
 //   kAny = false: closest hit in [tmin, tmax) with the tie rule.
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
 //   kQuant = true: the node records are DNodeQ (RT_NODES_QUANT8), else DNode4.
-template <bool kAny, bool kCount, bool kVol, bool kQuant = false>
+template <bool kAny, bool kCount, bool kVol, bool kQuant = false, bool kWide = false>
 __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
   // Reference-order mode (DScene.dfs_order; only in the rare-primitive kVol
   // variant, closest hit): scenes holding a RotateX / RotateZ wrapper, whose
@@ -976,6 +984,78 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
 #endif
     const float hi = kAny ? T.tmax : exact ? best_t(T) : T.bt;
     const float inf = __builtin_inff();
+    if constexpr (kWide) {
+      // 8-wide quantised node (DNode8, RT_NODES_WIDE8): five 16-B loads for
+      // eight children; near / far plane rows picked by load address (the
+      // direction's signs), the slab test in the RT_NODES_QUANT8 form; the
+      // hit children in octant order (slot oct ^ j for j = 0..7: roughly
+      // near to far, no sort); the first is visited, the others pushed.
+      const uint32_t nidx = GIX(T.item & ITEM_MASK, sc.n_nodes8, 62);
+      const uint32_t nb = nidx << 7;
+      const char* const nbase = reinterpret_cast<const char*>(sc.nodes8);
+      const uint32_t ux = __float_as_uint(T.cr.inv.x), uy = __float_as_uint(T.cr.inv.y), uz = __float_as_uint(T.cr.inv.z);
+      const uint32_t sxo = (ux >> 28) & 8u, syo = (uy >> 28) & 8u, szo = (uz >> 28) & 8u;
+      struct U4 { uint32_t x, y, z, w; };
+      auto ldu = [&](uint32_t off) {
+        const rtg_f4u v = *reinterpret_cast<const rtg_f4u*>(nbase + off);
+        return U4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+      };
+      const U4 h0 = ldu(nb), h1 = ldu(nb + 16u);
+      const U4 rx = ldu(nb + 32u + sxo), ry = ldu(nb + 56u + syo), rz = ldu(nb + 80u + szo);
+#if !defined(RTG_HOST_EMU)
+      // all five loads in flight together: the compiler otherwise issues the
+      // Y / Z rows only after waiting for the header (two round trips a step)
+      asm volatile("" ::"v"(h0.x), "v"(h0.y), "v"(h0.z), "v"(h0.w), "v"(h1.x), "v"(h1.y), "v"(h1.z), "v"(h1.w));
+      asm volatile("" ::"v"(rx.x), "v"(rx.y), "v"(rx.z), "v"(rx.w), "v"(ry.x), "v"(ry.y), "v"(ry.z), "v"(ry.w));
+      asm volatile("" ::"v"(rz.x), "v"(rz.y), "v"(rz.z), "v"(rz.w));
+#endif
+#ifdef RTG_STAMP
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      const float stx = __uint_as_float(h1.y & 0xFFFF0000u), sty = __uint_as_float(h1.y << 16),
+                  stz = __uint_as_float(h1.z & 0xFFFF0000u);
+      const float ax = (__uint_as_float(h0.x) - T.cr.o.x) * T.cr.inv.x, bx = T.cr.inv.x * stx;
+      const float ay = (__uint_as_float(h0.y) - T.cr.o.y) * T.cr.inv.y, by = T.cr.inv.y * sty;
+      const float az = (__uint_as_float(h0.z) - T.cr.o.z) * T.cr.inv.z, bz = T.cr.inv.z * stz;
+      const uint32_t oct = (ux >> 31) | ((uy >> 31) << 1) | ((uz >> 31) << 2);
+      uint32_t m = 0u;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t sh = 8u * uint32_t(c & 3);
+        auto qf = [sh](uint32_t row) { return float((row >> sh) & 0xFFu); };   // v_cvt_f32_ubyte<c & 3>
+        const uint32_t nx = c < 4 ? rx.x : rx.y, fx = c < 4 ? rx.z : rx.w;
+        const uint32_t ny = c < 4 ? ry.x : ry.y, fy = c < 4 ? ry.z : ry.w;
+        const uint32_t nz = c < 4 ? rz.x : rz.y, fz = c < 4 ? rz.z : rz.w;
+        const float tn = fmaxf(fmaxf(fmaxf(T.tmin, fmaf(qf(nx), bx, ax)), fmaf(qf(ny), by, ay)), fmaf(qf(nz), bz, az));
+        const float tf = fminf(fminf(fminf(hi, fmaf(qf(fx), bx, ax)), fmaf(qf(fy), by, ay)), fmaf(qf(fz), bz, az));
+        m |= (tf > tn ? 1u : 0u) << (uint32_t(c) ^ oct);
+      }
+      if (kCount) cnt.nodes++;
+      const uint32_t imask = (h1.z >> 8) & 0xFFu, lmask = h1.z & 0xFFu, twomask = h1.w & 0xFFu;
+      const bool trin = ((h1.w >> 8) & kNode8Tri) != 0u;
+      // branch-free: node child_base + rank among the internal slots; leaf
+      // leaf_base + rank among the leaf slots (+ the 2-triangle leaves
+      // below it in a tri node)
+      const uint32_t leaf_tag = trin ? ITEM_WTRI1 : ITEM_LREF, two = trin ? twomask : 0u;
+      auto child_item = [&](uint32_t slot) -> uint32_t {
+        const uint32_t bit = 1u << slot, below = bit - 1u;
+        const bool node = (imask & bit) != 0u;
+        const uint32_t base = node ? h0.w : h1.x + uint32_t(__builtin_popcount(two & below));
+        const uint32_t tag = node ? ITEM_NODE : leaf_tag + ((two >> slot) & 1u);
+        return (tag << ITEM_SHIFT) | (base + uint32_t(__builtin_popcount((node ? imask : lmask) & below)));
+      };
+      if (m == 0u) {
+        T.item = pop();
+      } else {
+        T.item = child_item(uint32_t(__builtin_ctz(m)) ^ oct);
+        // the others farthest first, so the nearest of them pops first
+        for (uint32_t rest = m & (m - 1u); rest != 0u;) {
+          const uint32_t j = 31u - uint32_t(__builtin_clz(rest));
+          rest &= ~(1u << j);
+          push(child_item(j ^ oct));
+        }
+      }
+    } else {
     const uint32_t nidx = GIX(T.item & ITEM_MASK, sc.n_nodes, 9);
     float t0, t1, t2, t3;
     uint4 it;
@@ -1044,6 +1124,26 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
 #ifdef RTG_STAMP
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+#if RTG_PK_SLAB && !defined(RTG_HOST_EMU)
+      // the 24 plane distances two children at a time: v_pk_add_f32 (with
+      // the origin negated and broadcast) + v_pk_mul_f32, the same IEEE
+      // operations per lane as the scalar form below, so t0..t3 are
+      // bit-identical; half the VALU issue of the slab arithmetic
+      typedef float pf2 __attribute__((ext_vector_type(2)));
+      auto pk = [](float a, float b) { pf2 r = {a, b}; return r; };
+      const pf2 ox = pk(T.cr.o.x, T.cr.o.x), oy = pk(T.cr.o.y, T.cr.o.y), oz = pk(T.cr.o.z, T.cr.o.z);
+      const pf2 ix = pk(T.cr.inv.x, T.cr.inv.x), iy = pk(T.cr.inv.y, T.cr.inv.y), iz = pk(T.cr.inv.z, T.cr.inv.z);
+      const pf2 nx01 = (pk(nx.x, nx.y) - ox) * ix, nx23 = (pk(nx.z, nx.w) - ox) * ix;
+      const pf2 fx01 = (pk(fx.x, fx.y) - ox) * ix, fx23 = (pk(fx.z, fx.w) - ox) * ix;
+      const pf2 ny01 = (pk(ny.x, ny.y) - oy) * iy, ny23 = (pk(ny.z, ny.w) - oy) * iy;
+      const pf2 fy01 = (pk(fy.x, fy.y) - oy) * iy, fy23 = (pk(fy.z, fy.w) - oy) * iy;
+      const pf2 nz01 = (pk(nz.x, nz.y) - oz) * iz, nz23 = (pk(nz.z, nz.w) - oz) * iz;
+      const pf2 fz01 = (pk(fz.x, fz.y) - oz) * iz, fz23 = (pk(fz.z, fz.w) - oz) * iz;
+      t0 = slab(nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x);
+      t1 = slab(nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y);
+      t2 = slab(nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x);
+      t3 = slab(nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y);
+#else
       auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
         return slab((nxp - T.cr.o.x) * T.cr.inv.x, (fxp - T.cr.o.x) * T.cr.inv.x, (nyp - T.cr.o.y) * T.cr.inv.y,
                     (fyp - T.cr.o.y) * T.cr.inv.y, (nzp - T.cr.o.z) * T.cr.inv.z, (fzp - T.cr.o.z) * T.cr.inv.z);
@@ -1052,6 +1152,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       t1 = child_t(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y);
       t2 = child_t(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z);
       t3 = child_t(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w);
+#endif
     }
     if (kCount) cnt.nodes++;
 #ifdef RTG_STAMP
@@ -1087,6 +1188,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       if (t1 < inf) push(i1);
       T.item = i0;
     }
+    }   // BVH4 node
     // leaving an instance with nothing postponed: restore the world ray inline
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END && T.lf == ITEM_NONE) {
       T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
@@ -1112,7 +1214,12 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const bool st_l = rtg_lead();
     const uint32_t sa = rtg_stamp();
 #endif
-    const uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
+    uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
+    if (kWide && tag == ITEM_LREF) {   // a leaf of a non-triangle 8-wide node: its item first
+      T.lf = sc.litems[GIX(idx, sc.n_litems, 63)];
+      tag = T.lf >> ITEM_SHIFT;
+      idx = T.lf & ITEM_MASK;
+    }
     const bool is_inst = tag == ITEM_INSTANCE || tag == ITEM_WINST;
     // One gather per round for the record the postponed item names (the
     // first two triangles of a triangle leaf, a world quad / sphere, a leaf
@@ -1123,6 +1230,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     // 128 B of slack at its end (upload_vec).
     const char* rec = reinterpret_cast<const char*>(sc.nodes);   // INST_END: no record, any readable line
     if (item_is_tri_leaf(tag)) rec = reinterpret_cast<const char*>(sc.tris + GIX(idx, sc.n_tris, 12));
+    else if (kWide && item_is_wtri_leaf(tag)) rec = reinterpret_cast<const char*>(sc.wtris + GIX(idx, sc.n_wtris, 64));
     else if (tag == ITEM_LEAF) rec = reinterpret_cast<const char*>(sc.leaves + GIX(idx, sc.n_leaves, 10));
     else if (tag == ITEM_WQUAD) rec = reinterpret_cast<const char*>(sc.quads + GIX(idx, sc.n_quads, 37));
     else if (tag == ITEM_WSPHERE) rec = reinterpret_cast<const char*>(sc.spheres + GIX(idx, sc.n_spheres, 38));
@@ -1131,23 +1239,30 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     const rtg_f4u g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4];
     rtg_f4u g5 = {0.0f, 0.0f, 0.0f, 0.0f}, g6 = g5;
     if (is_inst) { g5 = g[5]; g6 = g[6]; }
-    if (item_is_tri_leaf(tag)) {
+    bool any = false;
+    auto tri_one = [&](const DTri& tr, int pos) {
+      float t = 0.0f;
+      if (kCount) cnt.tri++;
+      if (!tri_t(tr, T.cr.o, T.cr.d, T.tmin, t)) return;
+      if (kAny) { any = any || t <= T.tmax; return; }
+      const int cref = S.cur_ref();
+      const bool world = cref < 0;
+      const int refpos = world ? pos : cref;
+      const int primpos = world ? 0 : (PRIM_IN_INST | pos);
+      if (accept_hit(sc, t, PK_TRI, refpos, primpos, T, S)) take_hit(T, S, t, PK_TRI, pos, refpos, primpos);
+    };
+    if (kWide && item_is_wtri_leaf(tag)) {
+      // a triangle leaf of an 8-wide tri node: one or two 40-B DWTri
+      // records (triangle + its index in the scene arrays) from the gather
+      tri_one(DTri{{g0.x, g0.y, g0.z}, {g0.w, g1.x, g1.y}, {g1.z, g1.w, g2.x}}, int(__float_as_uint(g2.y)));
+      if (kAny && any) return TRAV_ANYHIT;
+      if (tag != ITEM_WTRI1) tri_one(DTri{{g2.z, g2.w, g3.x}, {g3.y, g3.z, g3.w}, {g4.x, g4.y, g4.z}}, int(__float_as_uint(g4.w)));
+      if (kAny && any) return TRAV_ANYHIT;
+    } else if (item_is_tri_leaf(tag)) {
       // inline triangle leaf (BLAS, tested once): the first two triangles
       // come from the gather, any further ones (reference-topology leaves)
       // are loaded one at a time
       const int n = int(tag - ITEM_TRI1) + 1;
-      bool any = false;
-      auto tri_one = [&](const DTri& tr, int pos) {
-        float t = 0.0f;
-        if (kCount) cnt.tri++;
-        if (!tri_t(tr, T.cr.o, T.cr.d, T.tmin, t)) return;
-        if (kAny) { any = any || t <= T.tmax; return; }
-        const int cref = S.cur_ref();
-        const bool world = cref < 0;
-        const int refpos = world ? pos : cref;
-        const int primpos = world ? 0 : (PRIM_IN_INST | pos);
-        if (accept_hit(sc, t, PK_TRI, refpos, primpos, T, S)) take_hit(T, S, t, PK_TRI, pos, refpos, primpos);
-      };
       tri_one(DTri{{g0.x, g0.y, g0.z}, {g0.w, g1.x, g1.y}, {g1.z, g1.w, g2.x}}, int(idx));
       if (kAny && any) return TRAV_ANYHIT;
       if (n > 1) tri_one(DTri{{g2.y, g2.z, g2.w}, {g3.x, g3.y, g3.z}, {g3.w, g4.x, g4.y}}, int(idx) + 1);
@@ -1269,7 +1384,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
           if (T.item < ITEM_POP) push(T.item);
           push(ITEM_INST_END << ITEM_SHIFT);
           T.cr = orr; S.set_cur_ref(int(idx));
-          T.item = __float_as_uint(g2.w);   // BLAS root item
+          T.item = __float_as_uint(kWide ? g4.w : g2.w);   // BLAS root item (DInstEntry.root8 in the 8-wide format)
         }
       }
     } else {  // ITEM_INST_END: back to the world-space ray

@@ -16,6 +16,7 @@
 // left-first DFS order; BLAS primitives are laid out in that order too.  The
 // device tie rule (render.hip, Best/accept) uses them.
 #include "flatten.h"
+#include "node_quant.h"
 
 #include <algorithm>
 #include <array>
@@ -1242,6 +1243,202 @@ struct Flattener {
     for (size_t i = 0; i < n_tlas4; ++i)
       for (uint32_t& it : S.nodes4[i].item) it = inline_world_leaf(it);
   }
+  // ---- BVH2 -> 8-wide nodes (DNode8, RT_NODES_WIDE8).  The same SAH-optimal
+  // cut as collapse4 with up to eight child items per node (dp8_*: the least
+  // total area of the nodes below, k = 2..8).  A node's internal children
+  // get consecutive indices (child_base + rank), its leaves' items go to
+  // litems — or, when every leaf is a triangle leaf of at most two
+  // triangles, the triangles themselves are copied to wtris in leaf order —
+  // so the traversal computes every child's item from the node header
+  // (DNode8).  Child boxes are the BVH2 boxes, quantised conservatively
+  // (quantize_node8), so hits do not depend on the format.
+  std::vector<std::array<double, 9>> dp8_cost;
+  std::vector<std::array<int8_t, 9>> dp8_split;
+  std::vector<uint8_t> dp8_done;
+  std::vector<int32_t> need8;
+  std::map<uint32_t, uint32_t> root8_memo;   // BVH2 root node -> 8-wide root item (shared BLASes)
+  std::map<uint32_t, int> root8_need;
+  double dp8_item(uint32_t item, int k) {
+    if ((item >> ITEM_SHIFT) != ITEM_NODE) return k == 1 ? 0.0 : std::numeric_limits<double>::infinity();
+    dp8_node(item & ITEM_MASK);
+    return dp8_cost[item & ITEM_MASK][k];
+  }
+  void dp8_node(uint32_t n2) {
+    if (dp8_done[n2]) return;
+    const DNode nd = S.nodes[n2];
+    std::array<double, 9> c;
+    std::array<int8_t, 9> s{};
+    c.fill(std::numeric_limits<double>::infinity());
+    for (int k = 2; k <= 8; ++k)
+      for (int a = 1; a < k; ++a) {
+        const double v = dp8_item(nd.litem, a) + dp8_item(nd.ritem, k - a);
+        if (v < c[k]) { c[k] = v; s[k] = int8_t(a); }
+      }
+    float box[6];
+    for (int i = 0; i < 6; i += 2) { box[i] = std::min(nd.l[i], nd.r[i]); box[i + 1] = std::max(nd.l[i + 1], nd.r[i + 1]); }
+    int kb = 2;
+    for (int k = 3; k <= 8; ++k)
+      if (c[k] < c[kb]) kb = k;
+    c[1] = half_area(box) + c[kb];
+    s[1] = int8_t(kb);
+    dp8_cost[n2] = c;
+    dp8_split[n2] = s;
+    dp8_done[n2] = 1;
+  }
+  void dp8_frontier(uint32_t item, const float* box, int k, Ch* out, int& nc) {
+    if (k == 1) { out[nc].item = item; std::copy(box, box + 6, out[nc].box); ++nc; return; }
+    const DNode& nd = S.nodes[item & ITEM_MASK];
+    const int a = dp8_split[item & ITEM_MASK][k];
+    dp8_frontier(nd.litem, nd.l, a, out, nc);
+    dp8_frontier(nd.ritem, nd.r, k - a, out, nc);
+  }
+  // Octant slots: slot bit k set = the child's centre lies on the + side of
+  // the node's centre on axis k (offsets scaled by the node's extent);
+  // greedy: the best (child, slot) pair first.
+  static void assign_slots8(const Ch* ch, int nc, int* slot_of) {
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (int c = 0; c < nc; ++c)
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = std::min(lo[a], double(ch[c].box[2 * a]));
+        hi[a] = std::max(hi[a], double(ch[c].box[2 * a + 1]));
+      }
+    double off[8][3];
+    for (int c = 0; c < nc; ++c)
+      for (int a = 0; a < 3; ++a) {
+        const double ext = hi[a] - lo[a];
+        const double d = 0.5 * (double(ch[c].box[2 * a]) + double(ch[c].box[2 * a + 1])) - 0.5 * (lo[a] + hi[a]);
+        off[c][a] = std::isfinite(d) && std::isfinite(ext) && ext > 0.0 ? d / ext : 0.0;
+      }
+    bool cdone[8] = {}, sdone[8] = {};
+    for (int n = 0; n < nc; ++n) {
+      int bc = -1, bs = -1;
+      double best = HUGE_VAL;
+      for (int c = 0; c < nc; ++c) {
+        if (cdone[c]) continue;
+        for (int s = 0; s < 8; ++s) {
+          if (sdone[s]) continue;
+          double cost = 0.0;
+          for (int a = 0; a < 3; ++a) cost -= ((s >> a) & 1 ? 1.0 : -1.0) * off[c][a];
+          if (cost < best) { best = cost; bc = c; bs = s; }
+        }
+      }
+      cdone[bc] = sdone[bs] = true;
+      slot_of[bc] = bs;
+    }
+  }
+  // one 8-wide node from BVH2 node n2 at index idx (its children's block is
+  // allocated here, their nodes filled depth first)
+  void fill8(uint32_t idx, uint32_t n2, bool tlas) {
+    const DNode& nd = S.nodes[n2];
+    dp8_node(n2);
+    Ch ch[8];
+    int nc = 0;
+    const int k = dp8_split[n2][1], a = dp8_split[n2][k];
+    dp8_frontier(nd.litem, nd.l, a, ch, nc);
+    dp8_frontier(nd.ritem, nd.r, k - a, ch, nc);
+    int slot_of[8];
+    assign_slots8(ch, nc, slot_of);
+    int at[8];
+    bool used[8] = {};
+    for (int s = 0; s < 8; ++s) at[s] = -1;
+    for (int c = 0; c < nc; ++c) { at[slot_of[c]] = c; used[slot_of[c]] = true; }
+    uint32_t imask = 0, lmask = 0, twomask = 0;
+    uint32_t items[8] = {};
+    bool tri = true;
+    for (int s = 0; s < 8; ++s) {
+      if (!used[s]) continue;
+      const uint32_t it = ch[at[s]].item;
+      if ((it >> ITEM_SHIFT) == ITEM_NODE) { imask |= 1u << s; continue; }
+      lmask |= 1u << s;
+      uint32_t li = inline_leaf(it);
+      if (tlas) li = inline_world_leaf(li);
+      items[s] = li;
+      const uint32_t tag = li >> ITEM_SHIFT;
+      if (!(tag == ITEM_TRI1 || tag == ITEM_TRI1 + 1u)) tri = false;
+    }
+    if (lmask == 0) tri = false;
+    DNode8 o{};
+    o.child_base = uint32_t(S.nodes8.size());
+    const int ni = __builtin_popcount(imask);
+    S.nodes8.resize(S.nodes8.size() + size_t(ni));
+    need8.resize(S.nodes8.size(), 0);
+    o.leaf_base = uint32_t(tri ? S.wtris.size() : S.litems.size());
+    for (int s = 0; s < 8; ++s) {
+      if (!(lmask >> s & 1u)) continue;
+      if (tri) {
+        const uint32_t first = items[s] & ITEM_MASK;
+        const int n = int((items[s] >> ITEM_SHIFT) - ITEM_TRI1) + 1;
+        if (n == 2) twomask |= 1u << s;
+        for (int j = 0; j < n; ++j) {
+          const DTri& t = S.tris[first + uint32_t(j)];
+          DWTri w;
+          std::copy(t.v0, t.v0 + 3, w.v0);
+          std::copy(t.e1, t.e1 + 3, w.e1);
+          std::copy(t.e2, t.e2 + 3, w.e2);
+          w.tri = int32_t(first) + j;
+          S.wtris.push_back(w);
+        }
+      } else {
+        S.litems.push_back(items[s]);
+      }
+    }
+    float boxes[8][6] = {};
+    for (int s = 0; s < 8; ++s)
+      if (used[s]) std::copy(ch[at[s]].box, ch[at[s]].box + 6, boxes[s]);
+    uint32_t sb[3];
+    quantize_node8(boxes, used, o.org, sb, o.q);
+    o.sxy = (sb[0] & 0xFFFF0000u) | (sb[1] >> 16);
+    o.sz_masks = (sb[2] & 0xFFFF0000u) | (imask << 8) | lmask;
+    o.meta = twomask | ((tri ? kNode8Tri : 0u) << 8);
+    S.nodes8[idx] = o;
+    int worst = 0, r = 0;
+    for (int s = 0; s < 8; ++s) {
+      if (!(imask >> s & 1u)) continue;
+      const uint32_t ci = o.child_base + uint32_t(r++);
+      fill8(ci, ch[at[s]].item & ITEM_MASK, tlas);
+      worst = std::max(worst, int(need8[ci]));
+    }
+    need8[idx] = (nc - 1) + worst;
+  }
+  uint32_t build8(uint32_t root2, bool tlas, int& need) {
+    need = 0;
+    if ((root2 >> ITEM_SHIFT) != ITEM_NODE) {
+      // a leaf root: the world's is converted like a node's leaf child, a
+      // BLAS root keeps its DLeaf (as collapse4 does)
+      return tlas ? inline_world_leaf(inline_leaf(root2)) : root2;
+    }
+    const uint32_t n2 = root2 & ITEM_MASK;
+    auto m = root8_memo.find(n2);
+    if (m != root8_memo.end()) { need = root8_need[n2]; return m->second; }
+    const uint32_t idx = uint32_t(S.nodes8.size());
+    S.nodes8.emplace_back();
+    need8.resize(S.nodes8.size(), 0);
+    fill8(idx, n2, tlas);
+    need = need8[idx];
+    const uint32_t item = (ITEM_NODE << ITEM_SHIFT) | idx;
+    root8_memo[n2] = item;
+    root8_need[n2] = need;
+    return item;
+  }
+  // tlas2 / blas2: the BVH2 root items (build_bvh4 replaces the headers' own)
+  void build_bvh8(uint32_t tlas2, const std::vector<uint32_t>& blas2) {
+    dp8_cost.assign(S.nodes.size(), {});
+    dp8_split.assign(S.nodes.size(), {});
+    dp8_done.assign(S.nodes.size(), 0);
+    S.nodes8.clear(); S.litems.clear(); S.wtris.clear();
+    need8.clear();
+    int n = 0;
+    S.root8 = build8(tlas2, true, n);
+    S.tlas_need8 = n;
+    S.blas_root8.assign(blas2.size(), 0u);
+    S.blas_need8 = 0;
+    for (size_t b = 0; b < blas2.size(); ++b) {
+      S.blas_root8[b] = build8(blas2[b], false, n);
+      S.blas_need8 = std::max(S.blas_need8, n);
+    }
+    S.stack_needed8 = S.tlas_need8 + max_leaf_inst + 1 + S.blas_need8 + 2;
+  }
+
   uint32_t inline_world_leaf(uint32_t item) {
     if ((item >> ITEM_SHIFT) != ITEM_LEAF || item == empty_leaf) return item;
     const DLeaf& L = S.leaves[item & ITEM_MASK];
@@ -1312,6 +1509,10 @@ struct Flattener {
     lights();
     if (status) return status;
     environment();
+    // the BVH2 roots, before build_bvh4 points the headers at BVH4 nodes
+    const uint32_t tlas2 = S.tlas.root_item;
+    std::vector<uint32_t> blas2;
+    for (const DBvh& b : S.blas) blas2.push_back(b.root_item);
     build_bvh4();
     // stack: pending siblings along the worst world path + pending instances
     // in a leaf + the pending item and INST_END marker of an instance entry +
@@ -1320,7 +1521,7 @@ struct Flattener {
     // RotateX/RotateZ bboxes do not contain what Hit sees (transform.go:201-351):
     // which rays reach those objects depends on the exact node boxes, so such
     // scenes keep the fp32 DNode4 boxes whatever node format was asked for
-    S.quant_nodes = opt.quant_nodes && tlas_sah_ok() ? 1 : 0;
+    S.quant_nodes = opt.quant_nodes == 1 && tlas_sah_ok() ? 1 : 0;
     S.stack_needed = S.tlas_need4 + max_leaf_inst + 1 + S.blas_need4 + 2;
     // the same scenes traverse in the reference's DFS order with exact box
     // culls (trav_step's reference-order mode), which keeps each stack
@@ -1328,6 +1529,18 @@ struct Flattener {
     S.dfs_order = tlas_sah_ok() ? 0 : 1;
     if (S.dfs_order) S.stack_needed *= 2;
     if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
+    // RT_NODES_WIDE8: only for scenes the 8-wide traversal runs (not the
+    // rare-primitive variant: no reference-order mode, no circles, no volume
+    // left in the world BVH) and whose BLASes are all built here
+    bool has_circle = false;
+    for (int i = 0; i < d->num_hittables; ++i) has_circle = has_circle || d->hittables[i].kind == RT_CIRCLE;
+    if (opt.quant_nodes == 2 && !S.dfs_order && !has_circle && S.volumes.size() == S.vol_refs.size() &&
+        S.device_builds.empty()) {
+      build_bvh8(tlas2, blas2);
+      S.wide_nodes = S.stack_needed8 <= kStackMax8 && S.nodes8.size() < (1u << 27) && S.litems.size() < (1u << 27) &&
+                     S.wtris.size() < (1u << 27);
+      if (!S.wide_nodes) { S.nodes8.clear(); S.litems.clear(); S.wtris.clear(); S.blas_root8.clear(); }
+    }
     if (S.refs.size() >= (1u << 27) || S.tris.size() >= (1u << 27) || S.nodes.size() >= (1u << 27) || S.nodes4.size() >= (1u << 27))
       fail(RT_ERR_UNSUPPORTED, "scene too large for 28-bit indices");
     // BVH4 node addresses are 32-bit byte offsets (index << 7, trav_step):
@@ -1357,6 +1570,7 @@ void build_inst_entries(HostScene& S) {
       e.rlo[a] = bb.box[2 * a]; e.rhi[a] = bb.box[2 * a + 1];
     }
     e.root_item = bb.root_item;
+    e.root8 = S.wide_nodes ? S.blas_root8[size_t(in.blas)] : 0u;
     e.check_box = bb.check_box;
     e.nwrap = in.nwrap;
     e.kinds = 0;

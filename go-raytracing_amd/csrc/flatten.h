@@ -53,6 +53,17 @@ struct HostScene {
   int tlas_need4 = 0, blas_need4 = 0;   // BVH4 stack entries along the worst root-to-leaf path
   int max_leaf_inst = 0;                 // most instances in one world leaf (stack bound)
   int quant_nodes = 0;                   // the traversal reads DNodeQ (RT_NODES_QUANT8, no RotateX/Z)
+  // 8-wide nodes (RT_NODES_WIDE8): built beside nodes4 when asked for and
+  // the scene takes them (no RotateX/Z, circles or volumes left in the world
+  // BVH, no device-built BLAS): the traversal kernels without the
+  // rare-primitive variant read them
+  int wide_nodes = 0;
+  std::vector<DNode8> nodes8;
+  std::vector<uint32_t> litems;
+  std::vector<DWTri> wtris;
+  uint32_t root8 = 0;                    // world BVH root item (8-wide)
+  std::vector<uint32_t> blas_root8;      // per BLAS: root item (8-wide; DInstEntry.root8)
+  int tlas_need8 = 0, blas_need8 = 0, stack_needed8 = 0;
   int dfs_order = 0;                     // RotateX/Z scenes: reference-order closest hit (trav_step); two stack words per entry
   // Mesh BLASes left to the device builder (RT_BLAS_DEVICE): their triangles
   // are in the arrays in reference DFS order; the BLAS header's root item is
@@ -76,7 +87,8 @@ struct FlattenOptions {
   int blas_builder = BLAS_SAH;
   int tlas_builder = BLAS_SAH;   // world BVH: SAH over the top-level objects, one per leaf
   int sah_min_prims = 16;   // smaller all-triangle BLASes keep the reference topology
-  int quant_nodes = 0;      // RT_NODES_QUANT8: the traversal reads DNodeQ (node_quant.h)
+  int quant_nodes = 0;      // RT_OPT_NODE_FORMAT: 0 fp32 DNode4, 1 RT_NODES_QUANT8 (DNodeQ, node_quant.h),
+                            // 2 RT_NODES_WIDE8 (DNode8, when the scene takes it; else DNode4)
   // Volumes are kept out of the world BVH and tested by k_shade (DVolRef),
   // so the traversal kernels carry no volume code; only in scenes without
   // circles (the traversal's rare-primitive variant would carry both).
@@ -99,6 +111,10 @@ std::vector<DVolRec> build_vol_recs(const HostScene& S);
 // Returns RT_OK or an rt_status; `err` receives a message.
 int flatten_scene(const rt_scene_desc* desc, HostScene& out, std::string& err,
                   const FlattenOptions& opt = FlattenOptions());
+
+// Traversal stack bound of the 8-wide format (more entries per level than
+// BVH4: up to seven siblings pushed per node); deeper scenes use DNode4.
+constexpr int kStackMax8 = 128;
 
 // fp64 -> fp32 with outward rounding (bbox lower / upper bounds).
 float round_down(double x);

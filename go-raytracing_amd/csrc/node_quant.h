@@ -21,6 +21,7 @@
 #pragma once
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "dev_layout.h"
 
@@ -97,6 +98,77 @@ __host__ __device__ inline DNodeQ quantize_node(const DNode4& n) {
     q.q[2 * a + 1] = rhi;
   }
   return q;
+}
+
+// The same quantiser for the 8-wide node (DNode8, RT_NODES_WIDE8), whose
+// steps are stored as bf16 (the upper half of an fp32): a step is rounded up
+// to 8 significant bits, which can only widen the grid, and the bytes are
+// then chosen on that grid exactly as above (the largest q with org + q step
+// <= lo - m, the smallest with org + q step >= hi + m), so every child box
+// holds its fp32 box plus the margin.  box[s] = {xlo, xhi, ylo, yhi, zlo,
+// zhi} of slot s; used[s] false = an unused slot (lo 255, hi 0 on every
+// axis).  Writes org, the three bf16 steps and the 18 plane words.
+__host__ __device__ inline uint32_t nq_bf16_up(float f) {   // f >= 0: bits of the smallest bf16 >= f
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  if (b & 0xFFFFu) b = (b + 0x10000u) & 0xFFFF0000u;
+  return b;
+}
+__host__ __device__ inline void quantize_node8(const float (*box)[6], const bool* used, float org[3], uint32_t step_bits[3],
+                                               uint32_t q[18]) {
+  double M = 0.0;
+  for (int s = 0; s < 8; ++s)
+    if (used[s])
+      for (int k = 0; k < 6; ++k)
+        if (fabs(double(box[s][k])) <= 0x1p96) M = fmax(M, fabs(double(box[s][k])));
+  const double m = fmax(ldexp(M, -17), 0x1p-60);
+  for (int a = 0; a < 3; ++a) {
+    double L = HUGE_VAL, U = -HUGE_VAL;
+    bool coarse = false, any = false;
+    for (int s = 0; s < 8; ++s) {
+      if (!used[s]) continue;
+      const double l = box[s][2 * a], h = box[s][2 * a + 1];
+      if (!(fabs(l) <= 0x1p96) || !(fabs(h) <= 0x1p96)) coarse = true;
+      if (l < L) L = l;
+      if (h > U) U = h;
+      any = true;
+    }
+    float o = 0.0f;
+    uint32_t sb = 0x3F800000u;   // 1.0
+    if (coarse) {
+      o = -0x1p107f;
+      sb = 0x71800000u;          // 2^100 (exact in bf16)
+    } else if (any) {
+      o = nq_round_down(L - m);
+      sb = nq_bf16_up(nq_round_up(fmax((U + m - double(o)) / 255.0, 0x1p-100)));
+    }
+    float st;
+    memcpy(&st, &sb, 4);
+    uint32_t lo[2] = {0u, 0u}, hi[2] = {0u, 0u};
+    for (int s = 0; s < 8; ++s) {
+      uint32_t bl = 255u, bh = 0u;   // unused slot: rejected on every axis
+      if (used[s] && coarse) {
+        bl = 0u;
+        bh = 255u;
+      } else if (used[s]) {
+        const double tl = double(box[s][2 * a]) - m, th = double(box[s][2 * a + 1]) + m;
+        double ql = floor((tl - double(o)) / double(st));
+        double qh = ceil((th - double(o)) / double(st));
+        if (ql < 0.0) ql = 0.0;
+        if (qh > 255.0) qh = 255.0;
+        while (ql > 0.0 && double(o) + ql * double(st) > tl) ql -= 1.0;
+        while (qh < 255.0 && double(o) + qh * double(st) < th) qh += 1.0;
+        bl = uint32_t(ql);
+        bh = uint32_t(qh);
+      }
+      lo[s >> 2] |= bl << (8 * (s & 3));
+      hi[s >> 2] |= bh << (8 * (s & 3));
+    }
+    org[a] = o;
+    step_bits[a] = sb;
+    uint32_t* r = q + 6 * a;   // lo, hi, lo: a 16-B window at +0 or +8 is (near, far)
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = hi[0]; r[3] = hi[1]; r[4] = lo[0]; r[5] = lo[1];
+  }
 }
 
 }  // namespace rtg

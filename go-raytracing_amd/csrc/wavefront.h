@@ -61,7 +61,9 @@ enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT =
 
 // Traversal kernels: LDS stack ring of kLdsStack entries per lane, the rest
 // of the depth (up to kStackMax) spills to global memory.
-constexpr int kStackMax = 64;
+// 128 covers the 8-wide format's bound (flatten.h kStackMax8; BVH4 scenes
+// need at most 64, the probe kernels' LDS stack).
+constexpr int kStackMax = 128;
 constexpr int kSpillLanesPerCU = 2048;   // max resident threads per CU
 
 struct WavePlan {

@@ -251,7 +251,7 @@ __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_
 // that finishes starts its next ray on the following step without waiting.
 // kFirst: bounce 0, the rays are the camera rays of the claimed slots (the
 // prefetch loads only the slot's pixel; GetRay runs when the ray starts).
-template <int STACK, bool kCount, bool kVol, bool kFirst, bool kQuant = false>
+template <int STACK, bool kCount, bool kVol, bool kFirst, bool kQuant = false, bool kWide = false>
 __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_extend(DScene sc, DCamera cam, WaveArgs a,
                                                                 PathStream cs, const uint32_t* count,
                                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
         po = make_float4(ro.x, ro.y, ro.z, 0.0f);
         pd = make_float4(rd.x, rd.y, rd.z, asf(key));
       }
-      const int s = trav_init<false, kCount>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), ray_time(asu(pd.w)),
+      const int s = trav_init<false, kCount, kWide>(sc, T, S, mk(po.x, po.y, po.z), mk(pd.x, pd.y, pd.z), ray_time(asu(pd.w)),
                                              0.001f, __builtin_inff(), asu(pd.w), pb, DOM_VOL, cnt);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<false, kCount, kVol, kQuant>(sc, T, S, cnt, a.err);
+      const int s = trav_step<false, kCount, kVol, kQuant, kWide>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
   }
@@ -738,7 +738,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
 // the job's visibility bits go to sj_vis (k_nee_apply sums the visible
 // contributions in that order, camera.go:549-558).  Lanes prefetch their next
 // job as k_extend does.
-template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kQuant = false>
+template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kQuant = false, bool kWide = false>
 __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   uint32_t qinfo = 1u;
   auto start_ray = [&](int rr, V3 dir, float tmax) -> int {
     if (kCount) cnt.shadow++;
-    return trav_init<true, kCount>(sc, T, S, P, dir, 0.0f, 0.001f, tmax, key, info >> 8,
+    return trav_init<true, kCount, kWide>(sc, T, S, P, dir, 0.0f, 0.001f, tmax, key, info >> 8,
                                    rr == 0 ? DOM_VOL_SH_HDRI : DOM_VOL_SH_AREA, cnt);
   };
   // ray r of the current job ended with status s; true when the job is done
@@ -814,7 +814,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<true, kCount, kVol, kQuant>(sc, T, S, cnt, a.err);
+      const int s = trav_step<true, kCount, kVol, kQuant, kWide>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
   }
@@ -947,7 +947,7 @@ static hipError_t mark_end(const WavePlan& plan, hipStream_t st) {
 // compute units those waves free, so the tails overlap with work.  Each
 // pixel belongs to one twin and keeps its sample order: the frame is
 // bit-identical to a one-stream render.
-template <int STACK, bool kCount, bool kVol, bool kEnvIS, int kShade, bool kQuant>
+template <int STACK, bool kCount, bool kVol, bool kEnvIS, int kShade, bool kQuant, bool kWide>
 static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
                               const WavePlan& plan) {
   const int cus = plan.num_cus;
@@ -970,10 +970,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
       if (plan.max_blocks > 0 && plan.max_blocks < max_trav_blocks) max_trav_blocks = plan.max_blocks;
       auto cap = [&](int g) { return g < max_trav_blocks ? g : max_trav_blocks; };
       gsh[t] = grid_for((const void*)k_shade<kCount, kEnvIS, kShade, false>, 256, shade_lds, nslots, cus);
-      gsd[t] = cap(grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>, 256, 0, nslots, cus));
+      gsd[t] = cap(grid_for((const void*)k_shadow<STACK, kCount, kVol, kEnvIS, kQuant, kWide>, 256, 0, nslots, cus));
       gap[t] = grid_for((const void*)k_nee_apply<kEnvIS>, 256, 0, nslots, cus);
-      gext0[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, true, kQuant>, 256, 0, nslots, cus));
-      gext[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, false, kQuant>, 256, 0, nslots, cus));
+      gext0[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, true, kQuant, kWide>, 256, 0, nslots, cus));
+      gext[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, false, kQuant, kWide>, 256, 0, nslots, cus));
     }
     if (plan.bounces_run) *plan.bounces_run = 0;
     for (int b = 0; b < plan.max_depth; ++b) {
@@ -995,10 +995,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         if (offset && t == 1 && (e = hipStreamWaitEvent(st, plan.offset_ev, 0)) != hipSuccess) return e;
         if ((e = mark_begin(plan, uint8_t(KC_EXTEND | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
-          hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
+          hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant, kWide>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         else
-          hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant>), dim3(gext[t]), dim3(256), 0, st, sc, cam, a,
+          hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant, kWide>), dim3(gext[t]), dim3(256), 0, st, sc, cam, a,
                              a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         if (offset && t == 0 && (e = hipEventRecord(plan.offset_ev, st)) != hipSuccess) return e;
@@ -1017,7 +1017,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         // then resets the next extend's fetch counter itself
         if (nee) {
           if ((e = mark_begin(plan, uint8_t(KC_SHADOW | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
-          hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant>), dim3(gsd[t]), dim3(256), 0, st, sc, a,
+          hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant, kWide>), dim3(gsd[t]), dim3(256), 0, st, sc, a,
                              cnt_shadow, fetch_sh, fetch_ext);
           if ((e = mark_end(plan, st)) != hipSuccess) return e;
           RTG_LAUNCHED("k_shadow", b, st);
@@ -1085,30 +1085,36 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     // the kVol variants also carry the rare primitives (circles)
     // (and the reference-order closest hit of RotateX/Z scenes, DScene.dfs_order)
     const bool vol = sc.has_volumes != 0 || sc.n_circles > 0 || sc.dfs_order != 0;
-#define RUN3(S, C, V, E, Q)                                                          \
-  do {                                                                               \
-    if (shade == SHADE_FULL) e = run_batches<S, C, V, E, SHADE_FULL, Q>(sc, cam, as, sts, plan);        \
-    else if (shade == SHADE_VOL) e = run_batches<S, C, V, E, SHADE_VOL, Q>(sc, cam, as, sts, plan);     \
-    else if (shade == SHADE_MAT) e = run_batches<S, C, V, E, SHADE_MAT, Q>(sc, cam, as, sts, plan);     \
-    else e = run_batches<S, C, V, E, SHADE_LEAN, Q>(sc, cam, as, sts, plan);                            \
+#define RUN3(S, C, V, E, Q, W)                                                          \
+  do {                                                                                  \
+    if (shade == SHADE_FULL) e = run_batches<S, C, V, E, SHADE_FULL, Q, W>(sc, cam, as, sts, plan);        \
+    else if (shade == SHADE_VOL) e = run_batches<S, C, V, E, SHADE_VOL, Q, W>(sc, cam, as, sts, plan);     \
+    else if (shade == SHADE_MAT) e = run_batches<S, C, V, E, SHADE_MAT, Q, W>(sc, cam, as, sts, plan);     \
+    else e = run_batches<S, C, V, E, SHADE_LEAN, Q, W>(sc, cam, as, sts, plan);                            \
   } while (0)
-#define RUN2(S, C, V, Q)            \
-  do {                              \
-    if (envis) RUN3(S, C, V, true, Q); \
-    else RUN3(S, C, V, false, Q);   \
+#define RUN2(S, C, V, Q, W)               \
+  do {                                    \
+    if (envis) RUN3(S, C, V, true, Q, W); \
+    else RUN3(S, C, V, false, Q, W);      \
   } while (0)
-    // RT_NODES_QUANT8 scenes run the quantised-node traversal (its own kernels:
-    // the default fp32 kernels carry no trace of it)
-#define RUN(S, C, V)                            \
-  do {                                          \
-    if (quant) RUN2(S, C, V, true);             \
-    else RUN2(S, C, V, false);                  \
+    // RT_NODES_QUANT8 / RT_NODES_WIDE8 scenes run their node format's
+    // traversal (kernels of their own: the default fp32 kernels carry no
+    // trace of them); the 8-wide format has no rare-primitive variant
+    // (flatten builds it only for scenes that do not need one)
+#define RUN(S, C, V)                                                 \
+  do {                                                               \
+    if constexpr (!(V)) {                                            \
+      if (wide) { RUN2(S, C, V, false, true); break; }               \
+    }                                                                \
+    if (quant) RUN2(S, C, V, true, false);                           \
+    else RUN2(S, C, V, false, false);                                \
   } while (0)
     // the importance-sampled HDRI is a NEE light only beside an area light
     // (sampleLightMIS needs one, camera.go:502): without lights the kEnvIS
     // code is dead, and its registers spilled (C5: 34 VGPRs in bounce 0's
     // shading)
-    const bool envis = sc.env.valid && sc.env.use_is && sc.num_lights > 0, quant = sc.quant_nodes != 0;
+    const bool envis = sc.env.valid && sc.env.use_is && sc.num_lights > 0, quant = sc.quant_nodes != 0,
+               wide = sc.wide_nodes != 0;
     const int shade = sc.shade_kind;
 #if defined(RTG_RING24) && !defined(RTG_DIAG_RING)
 #define RTG_DIAG_RING 24
@@ -1120,7 +1126,9 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     (void)quant;
     (void)stack;
     if (count) return hipErrorNotSupported;
-    if (vol) RUN2(RTG_DIAG_RING, false, true, false); else RUN2(RTG_DIAG_RING, false, false, false);
+    if (vol) RUN2(RTG_DIAG_RING, false, true, false, false);
+    else if (wide) RUN2(RTG_DIAG_RING, false, false, false, true);
+    else RUN2(RTG_DIAG_RING, false, false, false, false);
 #else
     if (stack > 8) {
       if (vol) { if (count) RUN(16, true, true); else RUN(16, false, true); }

@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the RT_ABI_VERSION this binding was written against.
-const ABIVersion = 6 // RT_ABI_VERSION
+const ABIVersion = 7 // RT_ABI_VERSION
 
 // Hittable kinds (enum rt_hittable_kind).
 const (
@@ -104,6 +104,7 @@ const (
 	BuildDevice     int32 = 2 // RT_BLAS_DEVICE
 	NodesFP32       int32 = 0 // RT_NODES_FP32
 	NodesQuant8     int32 = 1 // RT_NODES_QUANT8
+	NodesWide8      int32 = 2 // RT_NODES_WIDE8
 	OptDealing      int32 = 10 // RT_OPT_DEALING
 	OptDealFirst    int32 = 11 // RT_OPT_DEAL_FIRST
 	DealStatic      int32 = 0  // RT_DEAL_STATIC
@@ -231,6 +232,8 @@ type SceneInfo struct {
 	TLASDepth   int32 `c:"tlas_depth"`
 	BLASDepth   int32 `c:"blas_depth"`
 	DeviceBytes int64 `c:"device_bytes"`
+	NodeFormat  int32 `c:"node_format"`
+	Nodes8      int32 `c:"nodes8"`
 }
 
 // Image is an ImageLoader's pixels (rt/image_loader.go:17-24): linear

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -243,6 +243,10 @@ typedef struct rt_scene_info {
   int32_t instances, blases, volumes, materials, textures, lights;
   int32_t stack_needed, tlas_depth, blas_depth;
   int64_t device_bytes;
+  int32_t node_format;  /* the RT_NODES_* format the traversal kernels read
+                           (RT_OPT_NODE_FORMAT, or RT_NODES_FP32 when the
+                           scene does not take the one asked for)          */
+  int32_t nodes8;       /* RT_NODES_WIDE8: 8-wide nodes (else 0)           */
 } rt_scene_info;
 
 typedef struct rt_ctx rt_ctx;
@@ -304,7 +308,14 @@ int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t ma
  *     closest hits equal the fp32 format's only within that envelope (every
  *     BASELINE scene is inside it).  Scenes holding a RotateX/RotateZ wrapper
  *     always use RT_NODES_FP32 (their node boxes decide which rays reach
- *     an object, transform.go:201-351).
+ *     an object, transform.go:201-351).  RT_NODES_WIDE8 = 8-wide nodes of
+ *     128 B (one cache line: eight children's 8-bit planes in one frame per
+ *     node, the RT_NODES_QUANT8 quantiser with bf16 steps, children visited
+ *     in octant order), collapsed from the same SAH BVH2 with the same
+ *     SAH-optimal cut; fewer, wider node steps per ray.  Taken by scenes
+ *     without RotateX/RotateZ, circles or volumes left in the world BVH and
+ *     whose BLASes are host-built (not RT_BLAS_DEVICE); others keep
+ *     RT_NODES_FP32.  Hits equal the fp32 format's within the same envelope.
  *   RT_OPT_VOLUMES: RT_VOLUMES_LIFTED (default) = Volume objects are kept
  *     out of the world BVH and tested by the shading kernel on every path
  *     ray and NEE shadow ray (same results: the volume test runs over the
@@ -350,7 +361,7 @@ enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9, RT_OPT_DEALING = 10, RT_OPT_DEAL_FIRST = 11 };
 enum { RT_DEAL_STATIC = 0, RT_DEAL_DYNAMIC = 1 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
-enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1 };
+enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1, RT_NODES_WIDE8 = 2 };
 enum { RT_VOLUMES_LIFTED = 0, RT_VOLUMES_IN_BVH = 1 };
 enum { RT_COLLAPSE_SAH = 0, RT_COLLAPSE_GREEDY = 1 };
 int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value);

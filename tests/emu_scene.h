@@ -42,6 +42,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   opt.width = width;
   opt.lucy_rings = 60;
   opt.lucy_cols = 80;
+  if (getenv("RTG_EMU_FULL_LUCY")) opt.lucy_rings = opt.lucy_cols = 0;   // the scene's own 280K-triangle mesh
   opt.asset_dir = asset_dir;
   char err[512] = {0};
   if (rts_scene_create(name, &opt, &E.scn, err, sizeof err) != 0) { fprintf(stderr, "%s\n", err); return 3; }
@@ -58,7 +59,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
     E.padded.push_back(std::move(b));
     return reinterpret_cast<const T*>(E.padded.back().data());
   };
-  E.padded.reserve(8);
+  E.padded.reserve(16);
   d.nodes = ptr(h.nodes4); d.leaves = ptr(h.leaves); d.refs = ptr(h.refs); d.ref_rank = ptr(h.ref_rank);
   d.ref_box = ptr(h.ref_box); d.spheres = ptr(h.spheres); d.quads = ptr(h.quads); d.tris = ptr(h.tris);
   d.tri_aux = ptr(h.tri_aux); d.circles = ptr(h.circles); d.circle_rank = ptr(h.circle_rank);
@@ -75,6 +76,13 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   for (size_t i = 0; i < h.tris.size(); ++i) E.tri_shade[i] = make_tri_shade(h.tris[i], h.tri_aux[i]);
   d.tri_shade = E.tri_shade.data();
   d.leaves = pad(h.leaves); d.tris = pad(h.tris); d.quads = pad(h.quads); d.spheres = pad(h.spheres);
+  // RT_NODES_WIDE8 (RTG_EMU_QUANT=2): the 8-wide arrays, as api.cpp uploads them
+  d.wide_nodes = h.wide_nodes;
+  d.root8 = h.root8;
+  if (h.wide_nodes) {
+    d.nodes8 = pad(h.nodes8); d.litems = pad(h.litems); d.wtris = pad(h.wtris);
+    d.n_nodes8 = uint32_t(h.nodes8.size()); d.n_litems = uint32_t(h.litems.size()); d.n_wtris = uint32_t(h.wtris.size());
+  }
   d.quad_wref = ptr(h.quad_wref); d.sphere_wref = ptr(h.sphere_wref);
   d.volumes = ptr(h.volumes); d.vol_refs = ptr(h.vol_refs); d.materials = ptr(h.materials); d.textures = ptr(h.textures);
   d.lights = ptr(h.lights); d.sphere_rank = ptr(h.sphere_rank); d.quad_rank = ptr(h.quad_rank);

@@ -138,3 +138,34 @@ def test_wavefront_kernels_quant8_nodes_match_oracle(wave, O, g, tmp_path, name,
     ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
     got = np.fromfile(out, np.float32).reshape(ref.shape)
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())
+
+
+@pytest.mark.parametrize("name,batch,wide", [("cornell-lucy", 1, 1), ("random", 0, 1), ("cornell-smoke", 0, 1),
+                                             ("hdri-nee", 0, 1), ("hdri-test", 0, 1), ("simple", 1, 1),
+                                             ("cornell", 0, 1), ("quads", 0, 1), ("checkered-spheres", 0, 1),
+                                             ("primitives", 1, 0), ("cornell-rotations", 0, 0)])
+def test_wavefront_kernels_wide8_nodes_match_oracle(wave, O, g, tmp_path, name, batch, wide):
+    """The host emulation with the 8-wide node format (RT_NODES_WIDE8,
+    DNode8: octant-ordered children, computed child items, triangle leaves
+    as DWTri records, litems for the others); scenes that need the
+    rare-primitive traversal (circles: primitives; RotateX/Z) keep BVH4
+    nodes (`wide` = which one the emulation ran).  Same oracle bar."""
+    spp, seed, width = 2, 77, 40
+    out = tmp_path / f"{name}.f32"
+    args = [wave, name, str(width), str(spp), str(seed), ASSETS, str(out)]
+    if batch:
+        args.append(str(batch))
+    env = _env()
+    env["RTG_EMU_QUANT"] = "2"
+    r = subprocess.run(args, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["wide"] == wide and (info["nodes8"] > 0) == bool(wide), info
+    kw = dict(width=width)
+    if name == "cornell-lucy":
+        kw.update(lucy_rings=60, lucy_cols=80)
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
+    got = np.fromfile(out, np.float32).reshape(ref.shape)
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())

@@ -69,7 +69,7 @@ def test_volume_with_mesh_boundary_refused(g, builder):
 
 
 def test_node_format_option(g):
-    """RT_OPT_NODE_FORMAT: only RT_NODES_FP32 / RT_NODES_QUANT8 are accepted;
+    """RT_OPT_NODE_FORMAT: only RT_NODES_FP32 / RT_NODES_QUANT8 / RT_NODES_WIDE8 are accepted;
     a quantised upload renders the same frame as the fp32 one on a scene
     whose hits sit well inside the boxes' margins (CornellBox, 4 spp), and a
     RotateX/Z scene silently keeps its fp32 nodes: its quant8 upload holds no
@@ -80,16 +80,22 @@ def test_node_format_option(g):
         with pytest.raises(g.RTError):
             c.set_option(g.RT_OPT_NODE_FORMAT, 7)
         frames, nbytes, nodes = {}, {}, {}
-        for fmt in ("fp32", "quant8"):
+        used = {}
+        for fmt in ("fp32", "quant8", "wide8"):
             c.set_node_format(fmt)
             for name in ("cornell", "cornell-rotations"):
                 s = g.Scene(name, width=48)
                 c.upload(s.desc)
                 info = c.info()
                 nbytes[fmt, name], nodes[name] = info.device_bytes, info.nodes
+                used[fmt, name] = info.node_format
                 frames[fmt, name], _ = c.render(s.camera, g.make_params(4, 5, seed=3))
         for name in ("cornell", "cornell-rotations"):
             assert np.array_equal(frames["fp32", name], frames["quant8", name]), name
+            assert np.array_equal(frames["fp32", name], frames["wide8", name]), name
+        # the 8-wide format is taken by CornellBox, not by the RotateX/Z scene
+        assert used["wide8", "cornell"] == g.RT_NODES_WIDE8 and used["wide8", "cornell-rotations"] == g.RT_NODES_FP32
+        assert used["quant8", "cornell"] == g.RT_NODES_QUANT8 and used["fp32", "cornell"] == g.RT_NODES_FP32
         assert nbytes["quant8", "cornell-rotations"] == nbytes["fp32", "cornell-rotations"]
         assert nbytes["quant8", "cornell"] >= nbytes["fp32", "cornell"] + 64 * nodes["cornell"]
     finally:

@@ -33,15 +33,20 @@ LIFTED, IN_BVH = 0, 1
 # (id, scene, constructor kwargs, samples probed, max share of diverged
 # paths, bounces probed (0: the scene's MaxDepth), volume placement)
 CASES = [
-    ("cornell-lucy", "cornell-lucy", dict(width=320, aspect=16.0 / 9.0), (0, 5), 2e-3, 0, LIFTED),  # C4, 280K mesh
-    ("cornell", "cornell", dict(width=128), (0, 5), 2e-3, 0, LIFTED),              # C3, fog + area light
-    ("cornell-in-bvh", "cornell", dict(width=96), (0,), 2e-3, 0, IN_BVH),          # C3, fog traversed in the BVH
-    ("random", "random", dict(width=192), (0, 5), 2e-3, 0, LIFTED),                # C2 to MaxDepth 50
-    ("hdri-test", "hdri-test", dict(width=192), (0, 3), 2e-2, 0, LIFTED),          # C5 to MaxDepth 20
-    ("cornell-smoke", "cornell-smoke", dict(width=96), (0,), 2e-3, 0, LIFTED),     # two lifted volumes
-    ("cornell-smoke-in-bvh", "cornell-smoke", dict(width=96), (0,), 2e-3, 0, IN_BVH),
-    ("cornell-rotations", "cornell-rotations", dict(width=96), (0,), 2e-3, 0, LIFTED),  # RotateX/Z, Scale chains
-    ("hdri-nee", "hdri-nee", dict(width=96), (0,), 2e-2, 0, LIFTED),               # HDRI IS + area light
+    ("cornell-lucy", "cornell-lucy", dict(width=320, aspect=16.0 / 9.0), (0, 5), 2e-3, 0, LIFTED, "fp32"),  # C4, 280K mesh
+    ("cornell", "cornell", dict(width=128), (0, 5), 2e-3, 0, LIFTED, "fp32"),              # C3, fog + area light
+    ("cornell-in-bvh", "cornell", dict(width=96), (0,), 2e-3, 0, IN_BVH, "fp32"),          # C3, fog in the BVH
+    ("random", "random", dict(width=192), (0, 5), 2e-3, 0, LIFTED, "fp32"),                # C2 to MaxDepth 50
+    ("hdri-test", "hdri-test", dict(width=192), (0, 3), 2e-2, 0, LIFTED, "fp32"),          # C5 to MaxDepth 20
+    ("cornell-smoke", "cornell-smoke", dict(width=96), (0,), 2e-3, 0, LIFTED, "fp32"),     # two lifted volumes
+    ("cornell-smoke-in-bvh", "cornell-smoke", dict(width=96), (0,), 2e-3, 0, IN_BVH, "fp32"),
+    ("cornell-rotations", "cornell-rotations", dict(width=96), (0,), 2e-3, 0, LIFTED, "fp32"),  # RotateX/Z, Scale
+    ("hdri-nee", "hdri-nee", dict(width=96), (0,), 2e-2, 0, LIFTED, "fp32"),               # HDRI IS + area light
+    # the 8-wide node format (RT_NODES_WIDE8) through the production kernels
+    ("cornell-lucy-wide8", "cornell-lucy", dict(width=320, aspect=16.0 / 9.0), (0,), 2e-3, 0, LIFTED, "wide8"),
+    ("random-wide8", "random", dict(width=192), (0,), 2e-3, 0, LIFTED, "wide8"),
+    ("hdri-test-wide8", "hdri-test", dict(width=192), (0,), 2e-2, 0, LIFTED, "wide8"),
+    ("cornell-wide8", "cornell", dict(width=96), (0,), 2e-3, 0, LIFTED, "wide8"),
 ]
 
 
@@ -49,7 +54,7 @@ def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def compare_paths(g, O, name, kw, samples, bounces=0, volumes=LIFTED):
+def compare_paths(g, O, name, kw, samples, bounces=0, volumes=LIFTED, nodes="fp32"):
     """Per bounce and sample: (alive paths, compared, diverged, id/t mismatches,
     NEE mismatches).  Raises nothing; the caller asserts."""
     s = g.Scene(name, **kw)
@@ -59,7 +64,9 @@ def compare_paths(g, O, name, kw, samples, bounces=0, volumes=LIFTED):
     rows = []
     try:
         c.set_option(g.RT_OPT_VOLUMES, g.RT_VOLUMES_IN_BVH if volumes == IN_BVH else g.RT_VOLUMES_LIFTED)
+        c.set_node_format(nodes)
         c.upload(s.desc)
+        assert c.info().node_format == {"fp32": g.RT_NODES_FP32, "wide8": g.RT_NODES_WIDE8}[nodes]
         lifted = c.info().volumes > 0
         for sample in samples:
             ot, op, ott, oray, onee = O.path_records(s.desc, cam, SEED, sample, nb, fp32=True, threads=16)
@@ -95,9 +102,9 @@ def compare_paths(g, O, name, kw, samples, bounces=0, volumes=LIFTED):
     return rows
 
 
-@pytest.mark.parametrize("cid,name,kw,samples,max_div,bounces,volumes", CASES, ids=[c[0] for c in CASES])
-def test_bounce_hits_and_shadow_rays_bit_exact(g, O, cid, name, kw, samples, max_div, bounces, volumes):
-    rows = compare_paths(g, O, name, kw, samples, bounces, volumes)
+@pytest.mark.parametrize("cid,name,kw,samples,max_div,bounces,volumes,nodes", CASES, ids=[c[0] for c in CASES])
+def test_bounce_hits_and_shadow_rays_bit_exact(g, O, cid, name, kw, samples, max_div, bounces, volumes, nodes):
+    rows = compare_paths(g, O, name, kw, samples, bounces, volumes, nodes)
     for r in rows:
         print(f"{cid} sample {r['sample']} bounce {r['bounce']}: alive {r['alive']} compared {r['compared']} "
               f"diverged {r['diverged']} shadow rays {r['shadow_rays']} hit mismatches {r['hit_mismatch']} "

@@ -24,7 +24,7 @@ namespace {
 
 constexpr int kRing = 4;
 
-template <bool kVol, bool kEnvIS, int kShade, bool kQuant>
+template <bool kVol, bool kEnvIS, int kShade, bool kQuant, bool kWide = false>
 void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_t spb, int max_depth, float* out) {
   uint32_t* cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
   uint32_t* cnt_shadow = a.counts + CNT_SHADOW;
@@ -38,16 +38,16 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
     for (int b = 0; b < max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
       if (b == 0) {
-        k_extend<kRing, false, kVol, true, kQuant>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
+        k_extend<kRing, false, kVol, true, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
                                            fetch_ext, s0);
         k_shade<false, kEnvIS, kShade, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       } else {
-        k_extend<kRing, false, kVol, false, kQuant>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
+        k_extend<kRing, false, kVol, false, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
                                             fetch_ext, s0);
         k_shade<false, kEnvIS, kShade, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
       }
       if (sc.num_lights > 0) {   // as run_batches: no lights, no NEE launches
-        k_shadow<kRing, false, kVol, kEnvIS, kQuant>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
+        k_shadow<kRing, false, kVol, kEnvIS, kQuant, kWide>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
         k_nee_apply<kEnvIS>(a, cnt_shadow);
       }
     }
@@ -110,6 +110,9 @@ int main(int argc, char** argv) {
   const bool vol = d.has_volumes != 0 || d.n_circles > 0 || d.dfs_order != 0, envis = d.env.valid && d.env.use_is;
 #define RUNQ(V, H, F)                                                  \
   do {                                                                 \
+    if constexpr (!(V)) {                                              \
+      if (d.wide_nodes) { run<V, H, F, false, true>(d, cam, a, spp, spb, E.max_depth, out.data()); break; } \
+    }                                                                  \
     if (d.quant_nodes) run<V, H, F, true>(d, cam, a, spp, spb, E.max_depth, out.data()); \
     else run<V, H, F, false>(d, cam, a, spp, spb, E.max_depth, out.data()); \
   } while (0)
@@ -131,6 +134,7 @@ int main(int argc, char** argv) {
   if (!f) return 5;
   fwrite(out.data(), sizeof(float), out.size(), f);
   fclose(f);
-  printf("{\"width\": %d, \"height\": %d, \"slots\": %zu, \"overflow\": %d}\n", cam.width, cam.height, S, err);
+  printf("{\"width\": %d, \"height\": %d, \"slots\": %zu, \"overflow\": %d, \"wide\": %d, \"nodes8\": %zu}\n", cam.width,
+         cam.height, S, err, d.wide_nodes, E.h.nodes8.size());
   return err ? 6 : 0;
 }

@@ -20,8 +20,9 @@ tag = sys.argv[1]
 d = json.loads(open(f"gpurun_out/ab_{tag}.json").read().strip().splitlines()[-1])
 w = d.get("work_per_sample") or {}
 k = d.get("kernels") or {}
-print(tag, d["value"], {n: v["ms_total"] for n, v in k.items()},
-      {n: w.get(n) for n in ("node_visits", "tri_tests", "instance_visits", "stack_spills") if n in w}, flush=True)
+print(tag, d["value"], d["config"].get("nodes"), d["config"].get("frame_sum"), {n: v["ms_total"] for n, v in k.items()},
+      {n: w.get(n) for n in ("node_visits", "tri_tests", "quad_tests", "instance_visits", "stack_spills") if n in w},
+      flush=True)
 PY
   done
 done

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Vector-memory pipeline counters (TA address unit, TD data unit, TCP vector
 # L1 and its address translation) of bench.py's default workload, one pass
-# per counter group, for each node format given (default: fp32 quant8).
+# per counter group, for each node format given (default: fp32 quant8;
+# NODES="fp32 wide8" for the 8-wide comparison).
 # Output: gpurun_out/pmc_tex/<nodes>/<pass>/; summarise with
 #   python3 tools/pmc_summary.py gpurun_out/pmc_tex/<nodes>
 set -e
@@ -20,4 +21,5 @@ for nodes in ${NODES:-fp32 quant8}; do
   run tcp1 TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum
   run tcp2 TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum
   run sq SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+  run valu SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 done
