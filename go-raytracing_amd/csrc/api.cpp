@@ -69,6 +69,8 @@ struct rt_ctx {
   size_t opt_slots = 0;
   int opt_refill = 0;
   int opt_blocks = 0;
+  int opt_tail = 0;                     // RT_OPT_TAIL: 0 automatic, 1 off, > 1 the rays-left threshold
+  bool probing = false;                 // path_probe: every bounce through the wavefront kernels
   int opt_streams = 0;            // RT_OPT_STREAMS: 1..kMaxTwins twins (0 = automatic: kDefaultTwins)
   // twins of the last render (render_wave): the second's stream, the join
   // events, and where each twin's hit records and pixels are
@@ -496,6 +498,19 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   plan.debug_sync = debug_sync;
   plan.probe_host = ctx->probe_pinned;
   plan.bounces_run = &ctx->bounces_run;
+  // the long-tail kernel (k_tail): when at most this many paths are left in
+  // a deep render without lights; RTGPU_TAIL_RAYS sets the automatic value
+  static const int env_tail = [] {
+    const char* e = getenv("RTGPU_TAIL_RAYS");
+    return e ? atoi(e) : -1;
+  }();
+  const int auto_tail = env_tail >= 0 ? env_tail : kTailRaysDefault;
+  plan.tail_rays = ctx->probing || ctx->opt_tail == 1 ? 0u : uint32_t(ctx->opt_tail > 1 ? ctx->opt_tail : auto_tail);
+  static const int env_tail_first = [] {
+    const char* e = getenv("RTGPU_TAIL_FIRST");
+    return e ? atoi(e) : kTailFirstDefault;
+  }();
+  plan.tail_first = env_tail_first;
   ctx->tev_used = 0;
   if (ctx->timing) {
     // worst case: 2 events per timed launch, 3 timed launches per bounce, per batch and twin
@@ -910,6 +925,11 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (key == RT_OPT_STREAMS) {
     if (value < 0 || value > kMaxTwins) return set_err(ctx, RT_ERR_INVALID, "streams must be 0 (default) or 1..4");
     ctx->opt_streams = value;
+    return RT_OK;
+  }
+  if (key == RT_OPT_TAIL) {
+    if (value < 0) return set_err(ctx, RT_ERR_INVALID, "bad tail option");
+    ctx->opt_tail = value;
     return RT_OK;
   }
   if (key == RT_OPT_MAX_BLOCKS) {
@@ -1461,7 +1481,11 @@ int path_probe(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sa
   if ((rc = ensure(ctx, ctx->accum, n * 3 * sizeof(float)))) return rc;
   if ((rc = ensure(ctx, ctx->probe, n * 40))) return rc;
   const rt_render_params p{1, bounce + 1, sample, seed, nullptr, 0, 0};
+  // the records of bounce k are read back from the wavefront kernels' arrays:
+  // no long-tail kernel (it carries paths in registers)
+  ctx->probing = true;
   rc = render_impl(ctx, cam, &p, static_cast<float*>(ctx->accum.p), ctx->stream, false, nullptr, nullptr);
+  ctx->probing = false;
   if (rc) return rc;
   int32_t* top = static_cast<int32_t*>(ctx->probe.p);
   int32_t* prim = top + n;

@@ -66,7 +66,14 @@ enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT =
 constexpr int kStackMax = 128;
 constexpr int kSpillLanesPerCU = 2048;   // max resident threads per CU
 
+// Deep renders without lights hand their last paths to one persistent
+// launch (k_tail) once at most this many are left (RT_OPT_TAIL).
+constexpr int kTailRaysDefault = 1 << 23;
+constexpr int kTailFirstDefault = 7;
+
 struct WavePlan {
+  uint32_t tail_rays;       // > 0: k_tail takes over at most this many paths left (no lights, depth > 8)
+  int32_t tail_first;       // an extra rays-left check after this bounce (the regular ones: 7, 11, 15, ...)
   uint32_t spp;
   uint32_t samples_per_batch;
   uint32_t sample_offset;

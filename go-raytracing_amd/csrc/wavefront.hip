@@ -363,6 +363,204 @@ __device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks,
   }
 }
 
+// Shading of one path at one bounce, after its closest hit (camera.go:443-518
+// from world.Hit on, sampleLightMIS's set-up :538-678): the miss colour /
+// emission added to Lout[slot], the scattered ray, the NEE jobs' inputs.
+// Shared by k_shade (block-compacted queues) and k_tail (one lane carries a
+// path to its end): the same operations in the same order either way.
+//   h: the hit record k_extend stores (t, kind << 28 | index, instance, ref)
+//   out: cont (a scattered ray to trace: P, sd, nbeta, nstate), want_shadow
+//   (NEE rays: flags, da / tmax_a / ca, dh / ch)
+template <bool kCount, bool kEnvIS, int kShade, bool kFirst>
+__device__ __forceinline__ void shade_path(const DScene& sc, const DCamera& cam, const WaveArgs& a, const DVolRec* vrecs,
+                                           const float4 h, const V3 ro, const V3 rd, const V3 beta, const uint32_t key,
+                                           const uint32_t slot, const int dleft, const uint32_t bounce, const bool allow,
+                                           bool& cont, bool& want_shadow, uint32_t& flags, uint32_t& nstate,
+                                           float& tmax_a, V3& P, V3& sd, V3& nbeta, V3& ca, V3& ch, V3& da, V3& dh,
+                                           bool& lout_set, Cnt& cnt) {
+  // L += beta * e on the path's radiance in Lout[slot] (camera.go:466, :481);
+  // adding an exact zero (black background) leaves L unchanged, so it is
+  // skipped.  At bounce 0 the radiance starts at 0 here (0 + beta * e).
+  auto add_L = [&](V3 e) {
+    if (e.x == 0.0f && e.y == 0.0f && e.z == 0.0f) return;
+    float4* lp = &a.Lout[GIX(slot, a.slots, 44)];
+    const float4 l4 = kFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ldnt(lp);
+    const V3 L = add(mk(l4.x, l4.y, l4.z), mul(beta, e));
+    stnt(lp, make_float4(L.x, L.y, L.z, 0.0f));
+    lout_set = true;
+  };
+  const float time = ray_time(key);
+  uint32_t kh = asu(h.y);
+  float ht = h.x;
+  int hinst = int(asu(h.z));
+#ifndef RTG_DIAG_NO_VOL   // diagnostic builds only: the shading kernel without its volume tests (wrong frames)
+  if (kShade == SHADE_VOL) {
+    int hrefpos = int(asu(h.w));
+    lifted_volumes<kCount>(sc, ro, rd, key, bounce, kh, ht, hinst, hrefpos, cnt, vrecs);
+  }
+#endif
+#ifdef RTG_GUARD
+  if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
+#endif
+  if (kh == 0u) {                                            // miss (camera.go:451-466)
+    V3 bg;
+    if (sc.env.valid) {
+      if (cam.phantom && dleft == cam.cam_max_depth) bg = mk(0.0f, 0.0f, 0.0f);
+      else { bg = env_sample(sc.env, rd); if (kCount) cnt.env++; }
+    } else if (cam.use_sky) {
+      V3 ud = unit(rd);
+      float aa = 0.5f * (ud.y + 1.0f);
+      bg = add(scale(mk(1.0f, 1.0f, 1.0f), 1.0f - aa), scale(mk(0.5f, 0.7f, 1.0f), aa));
+    } else {
+      bg = ld3(cam.background);
+    }
+    add_L(bg);
+  } else {
+    Best b{};
+    b.t = ht; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = hinst;
+    b.refpos = 0; b.primpos = 0;
+    Rec rec = make_record<kShade == SHADE_FULL>(sc, b, ro, rd, time);
+    P = rec.P;
+    const DMaterial& m = sc.materials[GIX(rec.mat, sc.num_materials, 42)];
+    if (kCount) cnt.mat++;
+    V3 att = mk(0.0f, 0.0f, 0.0f);
+    bool scat = true, use_mis = false;
+    if (m.kind == 4) {                                        // DiffuseLight
+      if (allow) add_L(tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P));
+      scat = false;
+    } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
+      sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
+      if (near_zero(sd)) sd = rec.N;
+      att = tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P);
+      use_mis = sc.num_lights > 0;
+    } else if (kShade == SHADE_LEAN) {
+      scat = false;                                           // unreachable: no such material
+    } else if (m.kind == 5) {                                 // Isotropic material.go:266-270
+      sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
+      att = tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P);
+    } else if (m.kind == 2) {                                 // Metal material.go:113-119
+      V3 refl = reflect(rd, rec.N);
+      refl = add(unit(refl), scale(random_unit_vector(key, bounce, DOM_SCATTER, 0), m.fuzz));
+      sd = refl;
+      att = ld3(m.albedo);
+      scat = dot(sd, rec.N) > 0.0f;
+    } else if (m.kind == 3) {                                 // Dielectric material.go:164-188
+      att = mk(1.0f, 1.0f, 1.0f);
+      float ri = rec.front ? (1.0f / m.ior) : m.ior;
+      V3 ud = unit(rd);
+      float c = dot(neg(ud), rec.N);
+      float ct = c < 1.0f ? c : 1.0f;
+      float stt = sqrtf(1.0f - ct * ct);
+      bool cannot = ri * stt > 1.0f;
+      bool refl = cannot;
+      if (!cannot) {
+        float r0 = (1.0f - ri) / (1.0f + ri);
+        r0 = r0 * r0;
+        float rf = r0 + (1.0f - r0) * pow5(1.0f - ct);
+        refl = rf > rnd(key, ctr(bounce, DOM_FRESNEL, 0));
+      }
+      sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
+    } else {
+      scat = false;                                           // unreachable: no such material
+    }
+    if (scat) {
+      if (use_mis) {                                          // camera.go:502-517 (set-up)
+        const int nl = sc.num_lights;
+        int li = int(rnd(key, ctr(bounce, DOM_NEE, 0)) * float(nl));
+        if (li >= nl) li = nl - 1;
+        if (kEnvIS && sc.env.valid && sc.env.use_is) {        // sampleHDRILight camera.go:565-607
+          const DEnv& e = sc.env;
+          V3 ldir, em;
+          float pdfH;
+          if (!(e.total_power > 0.0f)) {
+            ldir = random_unit_vector(key, bounce, DOM_NEE, 5);
+            em = env_sample(e, ldir);
+            pdfH = 1.0f / (4.0f * kPi);
+          } else {
+            float xi1 = rnd(key, ctr(bounce, DOM_NEE, 3));
+            int y = search_cdf(e.marginal, e.height, xi1);
+            float xi2 = rnd(key, ctr(bounce, DOM_NEE, 4));
+            int x = search_cdf(e.conditional + size_t(y) * (e.width + 1), e.width, xi2);
+            float uu = (float(x) + 0.5f) / float(e.width);
+            float vv = (float(y) + 0.5f) / float(e.height);
+            uu = uu - e.rotation / (2.0f * kPi);
+            uu = uu - floorf(uu);
+            float phi = (uu - 0.5f) * 2.0f * kPi;
+            float th = (0.5f - vv) * kPi;
+            float ctt = cosf(th);
+            ldir = mk(ctt * cosf(phi), sinf(th), ctt * sinf(phi));
+            em = texel(e, x, y);
+            pdfH = env_pdf(e, ldir);
+          }
+          float cth = dot(rec.N, ldir);
+          if (cth > 0.0f) {
+            float c2 = dot(rec.N, ldir);
+            float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
+            float w = pdfH / (pdfH + pdfB);
+            V3 ct = mul(scale(em, cth / pdfH * w), att);
+            ch = mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f));
+            dh = ldir;
+            flags |= 2u;
+          }
+        }
+        if (li < nl) {                                        // sampleAreaLight camera.go:610-678
+          const DLight& lt = sc.lights[li];
+          if (lt.is_quad) {
+            float al = rnd(key, ctr(bounce, DOM_NEE, 1)), be = rnd(key, ctr(bounce, DOM_NEE, 2));
+            V3 lp = add(add(ld3(lt.Q), scale(ld3(lt.u), al)), scale(ld3(lt.v), be));
+            V3 tl = sub(lp, rec.P);
+            float dist = len(tl);
+            V3 ldir = unit(tl);
+            float cth = dot(rec.N, ldir);
+            if (cth > 0.0f) {
+              const DMaterial& lm = sc.materials[lt.mat];
+              V3 em = lm.kind == 4 ? tex_value<kShade == SHADE_FULL>(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
+              float area = len(cross(ld3(lt.u), ld3(lt.v)));
+              float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
+              if (!(cl < 0.001f)) {
+                float pdfL = (dist * dist) / (cl * area);
+                float c2 = dot(rec.N, ldir);
+                float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
+                float w = pdfL / (pdfL + pdfB);
+                V3 ct = scale(mul(scale(em, cth / pdfL * w), att), float(nl));
+                ca = mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f));
+                da = ldir;
+                tmax_a = dist - 0.001f;
+                flags |= 1u;
+              }
+            }
+          }
+        }
+#ifdef RTG_DIAG_NO_VOL
+        if (false) {
+#else
+        if (kShade == SHADE_VOL && flags != 0u) {
+#endif
+          // a lifted volume occluding a shadow ray (camera.go:582, :639;
+          // the any-hit traversal's volume test, same interval and RNG
+          // domain) clears the ray: its contribution is not applied
+          for (int v = 0; v < sc.num_vol_refs; ++v) {
+            float tv = 0.0f;
+            const KVolRec R = kvolrec(vrecs, v);
+            const int nt = R->ref.ntests;
+            if ((flags & 2u) && volume_hit_rec<kCount>(R, P, dh, 0.001f, __builtin_inff(), nt, key, bounce,
+                                                       DOM_VOL_SH_HDRI, tv, cnt))
+              flags &= ~2u;
+            if ((flags & 1u) && volume_hit_rec<kCount>(R, P, da, 0.001f, tmax_a, nt, key, bounce,
+                                                       DOM_VOL_SH_AREA, tv, cnt))
+              flags &= ~1u;
+          }
+        }
+        want_shadow = flags != 0u;
+      }
+      nbeta = mul(beta, att);
+      const int nd = dleft - 1;
+      cont = nd > 0;
+      nstate = pack_state(nd, bounce + 1u, !use_mis);
+    }
+  }
+}
+
 // kEnvIS: the scene has an importance-sampled HDRI (sampleHDRILight set-up
 // compiled in); kShade (DScene.shade_kind): SHADE_LEAN = Lambertian /
 // DiffuseLight with solid or checker textures, SHADE_MAT = also Metal /
@@ -494,18 +692,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
     uint32_t slot = 0, key = 0, flags = 0, bounce = 0, nstate = 0;
     float tmax_a = 0.0f;
     V3 P = mk(0.0f, 0.0f, 0.0f), sd = P, beta = P, nbeta = P, ca = P, ch = P, da = P, dh = P;
-    // L += beta * e on the path's radiance in Lout[slot] (camera.go:466, :481);
-    // adding an exact zero (black background) leaves L unchanged, so it is
-    // skipped.  At bounce 0 the radiance starts at 0 here (0 + beta * e).
     bool lout_set = false;
-    auto add_L = [&](V3 e) {
-      if (e.x == 0.0f && e.y == 0.0f && e.z == 0.0f) return;
-      float4* lp = &a.Lout[GIX(slot, a.slots, 44)];
-      const float4 l4 = kFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ldnt(lp);
-      const V3 L = add(mk(l4.x, l4.y, l4.z), mul(beta, e));
-      stnt(lp, make_float4(L.x, L.y, L.z, 0.0f));
-      lout_set = true;
-    };
     if (live) {
       if (kCount) cnt.rays++;                                    // paths shaded
       const uint32_t ii = GIX(i, a.slots, 41);
@@ -532,176 +719,9 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
         rd = mk(d4.x, d4.y, d4.z);
         beta = mk(b4.x, b4.y, b4.z);
       }
-      const float time = ray_time(key);
-      uint32_t kh = asu(h.y);
-      float ht = h.x;
-      int hinst = int(asu(h.z));
-#ifndef RTG_DIAG_NO_VOL   // diagnostic builds only: the shading kernel without its volume tests (wrong frames)
-      if (kShade == SHADE_VOL) {
-        int hrefpos = int(asu(h.w));
-        lifted_volumes<kCount>(sc, ro, rd, key, bounce, kh, ht, hinst, hrefpos, cnt, vrecs);
-      }
-#endif
-#ifdef RTG_GUARD
-      if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
-#endif
-      if (kh == 0u) {                                            // miss (camera.go:451-466)
-        V3 bg;
-        if (sc.env.valid) {
-          if (cam.phantom && dleft == cam.cam_max_depth) bg = mk(0.0f, 0.0f, 0.0f);
-          else { bg = env_sample(sc.env, rd); if (kCount) cnt.env++; }
-        } else if (cam.use_sky) {
-          V3 ud = unit(rd);
-          float aa = 0.5f * (ud.y + 1.0f);
-          bg = add(scale(mk(1.0f, 1.0f, 1.0f), 1.0f - aa), scale(mk(0.5f, 0.7f, 1.0f), aa));
-        } else {
-          bg = ld3(cam.background);
-        }
-        add_L(bg);
-      } else {
-        Best b{};
-        b.t = ht; b.kind = int(kh >> 28); b.idx = int(kh & 0x0FFFFFFFu); b.inst = hinst;
-        b.refpos = 0; b.primpos = 0;
-        Rec rec = make_record<kShade == SHADE_FULL>(sc, b, ro, rd, time);
-        P = rec.P;
-        const DMaterial& m = sc.materials[GIX(rec.mat, sc.num_materials, 42)];
-        if (kCount) cnt.mat++;
-        V3 att = mk(0.0f, 0.0f, 0.0f);
-        bool scat = true, use_mis = false;
-        if (m.kind == 4) {                                        // DiffuseLight
-          if (allow) add_L(tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P));
-          scat = false;
-        } else if (m.kind == 1) {                                 // Lambertian material.go:57-68
-          sd = add(rec.N, random_unit_vector(key, bounce, DOM_SCATTER, 0));
-          if (near_zero(sd)) sd = rec.N;
-          att = tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P);
-          use_mis = sc.num_lights > 0;
-        } else if (kShade == SHADE_LEAN) {
-          scat = false;                                           // unreachable: no such material
-        } else if (m.kind == 5) {                                 // Isotropic material.go:266-270
-          sd = random_unit_vector(key, bounce, DOM_SCATTER, 0);
-          att = tex_value<kShade == SHADE_FULL>(sc, m.tex, rec.u, rec.v, rec.P);
-        } else if (m.kind == 2) {                                 // Metal material.go:113-119
-          V3 refl = reflect(rd, rec.N);
-          refl = add(unit(refl), scale(random_unit_vector(key, bounce, DOM_SCATTER, 0), m.fuzz));
-          sd = refl;
-          att = ld3(m.albedo);
-          scat = dot(sd, rec.N) > 0.0f;
-        } else if (m.kind == 3) {                                 // Dielectric material.go:164-188
-          att = mk(1.0f, 1.0f, 1.0f);
-          float ri = rec.front ? (1.0f / m.ior) : m.ior;
-          V3 ud = unit(rd);
-          float c = dot(neg(ud), rec.N);
-          float ct = c < 1.0f ? c : 1.0f;
-          float stt = sqrtf(1.0f - ct * ct);
-          bool cannot = ri * stt > 1.0f;
-          bool refl = cannot;
-          if (!cannot) {
-            float r0 = (1.0f - ri) / (1.0f + ri);
-            r0 = r0 * r0;
-            float rf = r0 + (1.0f - r0) * pow5(1.0f - ct);
-            refl = rf > rnd(key, ctr(bounce, DOM_FRESNEL, 0));
-          }
-          sd = refl ? reflect(ud, rec.N) : refract(ud, rec.N, ri);
-        } else {
-          scat = false;                                           // unreachable: no such material
-        }
-        if (scat) {
-          if (use_mis) {                                          // camera.go:502-517 (set-up)
-            const int nl = sc.num_lights;
-            int li = int(rnd(key, ctr(bounce, DOM_NEE, 0)) * float(nl));
-            if (li >= nl) li = nl - 1;
-            if (kEnvIS && sc.env.valid && sc.env.use_is) {        // sampleHDRILight camera.go:565-607
-              const DEnv& e = sc.env;
-              V3 ldir, em;
-              float pdfH;
-              if (!(e.total_power > 0.0f)) {
-                ldir = random_unit_vector(key, bounce, DOM_NEE, 5);
-                em = env_sample(e, ldir);
-                pdfH = 1.0f / (4.0f * kPi);
-              } else {
-                float xi1 = rnd(key, ctr(bounce, DOM_NEE, 3));
-                int y = search_cdf(e.marginal, e.height, xi1);
-                float xi2 = rnd(key, ctr(bounce, DOM_NEE, 4));
-                int x = search_cdf(e.conditional + size_t(y) * (e.width + 1), e.width, xi2);
-                float uu = (float(x) + 0.5f) / float(e.width);
-                float vv = (float(y) + 0.5f) / float(e.height);
-                uu = uu - e.rotation / (2.0f * kPi);
-                uu = uu - floorf(uu);
-                float phi = (uu - 0.5f) * 2.0f * kPi;
-                float th = (0.5f - vv) * kPi;
-                float ctt = cosf(th);
-                ldir = mk(ctt * cosf(phi), sinf(th), ctt * sinf(phi));
-                em = texel(e, x, y);
-                pdfH = env_pdf(e, ldir);
-              }
-              float cth = dot(rec.N, ldir);
-              if (cth > 0.0f) {
-                float c2 = dot(rec.N, ldir);
-                float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
-                float w = pdfH / (pdfH + pdfB);
-                V3 ct = mul(scale(em, cth / pdfH * w), att);
-                ch = mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f));
-                dh = ldir;
-                flags |= 2u;
-              }
-            }
-            if (li < nl) {                                        // sampleAreaLight camera.go:610-678
-              const DLight& lt = sc.lights[li];
-              if (lt.is_quad) {
-                float al = rnd(key, ctr(bounce, DOM_NEE, 1)), be = rnd(key, ctr(bounce, DOM_NEE, 2));
-                V3 lp = add(add(ld3(lt.Q), scale(ld3(lt.u), al)), scale(ld3(lt.v), be));
-                V3 tl = sub(lp, rec.P);
-                float dist = len(tl);
-                V3 ldir = unit(tl);
-                float cth = dot(rec.N, ldir);
-                if (cth > 0.0f) {
-                  const DMaterial& lm = sc.materials[lt.mat];
-                  V3 em = lm.kind == 4 ? tex_value<kShade == SHADE_FULL>(sc, lm.tex, 0.0f, 0.0f, lp) : mk(0.0f, 0.0f, 0.0f);
-                  float area = len(cross(ld3(lt.u), ld3(lt.v)));
-                  float cl = fabsf(dot(ld3(lt.n), neg(ldir)));
-                  if (!(cl < 0.001f)) {
-                    float pdfL = (dist * dist) / (cl * area);
-                    float c2 = dot(rec.N, ldir);
-                    float pdfB = c2 < 0.0f ? 0.0f : c2 / kPi;
-                    float w = pdfL / (pdfL + pdfB);
-                    V3 ct = scale(mul(scale(em, cth / pdfL * w), att), float(nl));
-                    ca = mk(gomin(ct.x, 20.0f), gomin(ct.y, 20.0f), gomin(ct.z, 20.0f));
-                    da = ldir;
-                    tmax_a = dist - 0.001f;
-                    flags |= 1u;
-                  }
-                }
-              }
-            }
-#ifdef RTG_DIAG_NO_VOL
-            if (false) {
-#else
-            if (kShade == SHADE_VOL && flags != 0u) {
-#endif
-              // a lifted volume occluding a shadow ray (camera.go:582, :639;
-              // the any-hit traversal's volume test, same interval and RNG
-              // domain) clears the ray: its contribution is not applied
-              for (int v = 0; v < sc.num_vol_refs; ++v) {
-                float tv = 0.0f;
-                const KVolRec R = kvolrec(vrecs, v);
-                const int nt = R->ref.ntests;
-                if ((flags & 2u) && volume_hit_rec<kCount>(R, P, dh, 0.001f, __builtin_inff(), nt, key, bounce,
-                                                           DOM_VOL_SH_HDRI, tv, cnt))
-                  flags &= ~2u;
-                if ((flags & 1u) && volume_hit_rec<kCount>(R, P, da, 0.001f, tmax_a, nt, key, bounce,
-                                                           DOM_VOL_SH_AREA, tv, cnt))
-                  flags &= ~1u;
-              }
-            }
-            want_shadow = flags != 0u;
-          }
-          nbeta = mul(beta, att);
-          const int nd = dleft - 1;
-          cont = nd > 0;
-          nstate = pack_state(nd, bounce + 1u, !use_mis);
-        }
-      }
+      shade_path<kCount, kEnvIS, kShade, kFirst>(sc, cam, a, vrecs, h, ro, rd, beta, key, slot, dleft, bounce, allow, cont,
+                                                 want_shadow, flags, nstate, tmax_a, P, sd, nbeta, ca, ch, da, dh,
+                                                 lout_set, cnt);
     }
     if (kFirst && live && !lout_set) stnt(&a.Lout[GIX(slot, a.slots, 44)], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     uint32_t jc = 0, js = 0;
@@ -731,6 +751,106 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
     }
   }
   if (kCount) add_counters(a.counters + KC_SHADE * CNT_BLOCK, cnt, 0);
+}
+
+// ---------------------------------------------------------------- tail
+// The long tail of deep renders without lights (RandomScene: MaxDepth 50,
+// HDRITestScene: 20).  Per bounce the wavefront schedule pays two launches
+// with their ramps however few paths are left (C2: about 0.19 ms per bounce
+// from bounce 10 on, 10 of its 119 ms).  Once few paths remain, run_batches
+// hands them to this one persistent launch instead: each lane takes a path
+// from the stream and carries it to its end, closest hit (trav_step) then
+// shade_path, bounce after bounce.  Every path goes through the same
+// operations in the same order as in k_extend / k_shade (the same RNG keys,
+// the same Lout[slot] adds), so the frame is bit-identical.  Scenes with
+// lights keep the wavefront schedule: their NEE jobs need k_shadow.
+#ifndef RTG_TAIL_WAVES
+#define RTG_TAIL_WAVES 4
+#endif
+template <int STACK, bool kVol, int kShade, bool kQuant, bool kWide>
+__global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+                                                              const uint32_t* count, uint32_t* fetch) {
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack ring + world ray + hit record
+#ifdef RTG_HOST_EMU
+  static char s_dyn[kLdsMaterials * sizeof(DMaterial) + kLdsTextures * sizeof(DTexture) + kLdsLights * sizeof(DLight)];
+#else
+  extern __shared__ char s_dyn[];   // shade_lds_bytes(sc), as k_shade
+#endif
+  DScene sc = scg;
+  if (kShade != SHADE_FULL || shade_tables_fit(sc)) {   // k_shade's LDS tables
+    DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
+    DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
+    DLight* const s_light = reinterpret_cast<DLight*>(s_tex + sc.num_textures);
+    for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = scg.materials[i];
+    for (int i = threadIdx.x; i < sc.num_textures; i += blockDim.x) s_tex[i] = scg.textures[i];
+    for (int i = threadIdx.x; i < sc.num_lights; i += blockDim.x) s_light[i] = scg.lights[i];
+    __syncthreads();
+    sc.materials = s_mat;
+    sc.textures = s_tex;
+    sc.lights = s_light;
+  }
+  const uint32_t n = *count;
+  const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
+#ifdef RTG_GUARD
+  if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(66, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
+#endif
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
+                 a.spill_cap};
+  Cnt cnt = {};
+  Trav T{};
+  Pool Q = pool_init();
+  uint32_t p = ITEM_NONE;   // the path this lane carries (its stream position)
+  V3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro, beta = ro;
+  uint32_t key = 0, slot = 0, st = 0;
+  bool pending = false;     // the lane's traversal has ended: shade it
+  auto start = [&]() {
+    const int s0 = trav_init<false, false, kWide>(sc, T, S, ro, rd, ray_time(key), 0.001f, __builtin_inff(), key,
+                                                  (st >> 16) & 0x7FFFu, DOM_VOL, cnt);
+    pending = s0 != TRAV_RUNNING;
+  };
+  for (;;) {
+    const uint32_t idx = pool_take(p == ITEM_NONE, Q, fetch, n, nwaves, 1);
+    if (idx != ITEM_NONE) {
+      p = GIX(idx, a.slots, 67);
+      const float4 o4 = ldnt(&cs.o[p]), d4 = ldnt(&cs.d[p]), b4 = ldnt(&cs.beta[p]);
+      ro = mk(o4.x, o4.y, o4.z);
+      rd = mk(d4.x, d4.y, d4.z);
+      beta = mk(b4.x, b4.y, b4.z);
+      key = asu(d4.w);
+      slot = asu(o4.w);
+      st = asu(b4.w);
+      start();
+    }
+    if (!__any(p != ITEM_NONE)) {
+      if (Q.dry) break;
+      continue;
+    }
+    if (p != ITEM_NONE && !pending) pending = trav_step<false, false, kVol, kQuant, kWide>(sc, T, S, cnt, a.err) != TRAV_RUNNING;
+    while (p != ITEM_NONE && pending) {
+      // the hit record k_extend would store (store_hit), then k_shade's shading
+      Best b = trav_best(T, S);
+      resolve_inst(sc, b);
+      const float4 h = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u),
+                                   asf(uint32_t(b.inst)), asf(uint32_t(b.refpos)));
+      bool cont = false, want_shadow = false, lout_set = false;
+      uint32_t flags = 0, nstate = 0;
+      float tmax_a = 0.0f;
+      V3 P = mk(0.0f, 0.0f, 0.0f), sd = P, nbeta = P, ca = P, ch = P, da = P, dh = P;
+      shade_path<false, false, kShade, false>(sc, cam, a, sc.vol_recs, h, ro, rd, beta, key, slot, int(st & 0xFFFFu),
+                                              (st >> 16) & 0x7FFFu, (st >> 31) != 0u, cont, want_shadow, flags, nstate,
+                                              tmax_a, P, sd, nbeta, ca, ch, da, dh, lout_set, cnt);
+      if (cont) {   // the next bounce of the same path (k_shade's survivor record)
+        ro = P;
+        rd = sd;
+        beta = nbeta;
+        st = nstate;
+        start();
+      } else {
+        p = ITEM_NONE;
+        pending = false;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- shadow
@@ -1025,7 +1145,7 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
           RTG_LAUNCHED("k_nee_apply", b, st);
         }
       }
-      if (plan.max_depth > 8 && b >= 7 && (b % 4) == 3) {
+      if (plan.max_depth > 8 && ((b >= 7 && (b % 4) == 3) || (plan.tail_rays > 0 && b == plan.tail_first))) {
         // long-tail scenes (RandomScene depth 50): stop once every path of
         // every twin ended
         for (int t = 0; t < nt; ++t)
@@ -1033,9 +1153,11 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
                                   hipMemcpyDeviceToHost, sts[t])) != hipSuccess)
             return e;
         uint32_t left = 0;
+        uint32_t lefts[kMaxTwins] = {};
         for (int t = 0; t < nt; ++t) {
           if ((e = hipStreamSynchronize(sts[t])) != hipSuccess) return e;
           left += plan.probe_host[t];
+          lefts[t] = plan.probe_host[t];
 #if RTG_TAIL_GRID
           // the counts only shrink from here: size the persistent grids for
           // what is left (every wave of a launch makes at least one claim
@@ -1050,6 +1172,23 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
 #endif
         }
         if (left == 0) break;
+        // few paths left in a render without lights: one k_tail launch per
+        // twin carries them to their ends (bit-identical frame)
+        if (!kCount && !nee && plan.tail_rays > 0 && left <= plan.tail_rays && b + 1 < plan.max_depth) {
+          const size_t lds = shade_lds_bytes(sc);
+          const int cap_tail = int(as[0].spill_lanes / 256u);
+          for (int t = 0; t < nt; ++t) {
+            if (lefts[t] == 0) continue;
+            const WaveArgs& a = as[t];
+            int g = grid_for((const void*)k_tail<STACK, kVol, kShade, kQuant, kWide>, 256, lds, lefts[t], cus);
+            if (g > cap_tail) g = cap_tail;
+            hipLaunchKernelGGL((k_tail<STACK, kVol, kShade, kQuant, kWide>), dim3(g), dim3(256), lds, sts[t], sc, cam, a,
+                               a.s[nx], a.counts + (nx ? CNT_STREAM1 : CNT_STREAM0), a.counts + CNT_FETCH_EXT);
+            RTG_LAUNCHED("k_tail", b + 1, sts[t]);
+          }
+          if (plan.bounces_run) *plan.bounces_run = plan.max_depth;
+          break;
+        }
       }
     }
     if (!kCount)

@@ -107,6 +107,7 @@ const (
 	NodesWide8      int32 = 2 // RT_NODES_WIDE8
 	OptDealing      int32 = 10 // RT_OPT_DEALING
 	OptDealFirst    int32 = 11 // RT_OPT_DEAL_FIRST
+	OptTail         int32 = 12 // RT_OPT_TAIL
 	DealStatic      int32 = 0  // RT_DEAL_STATIC
 	DealDynamic     int32 = 1  // RT_DEAL_DYNAMIC
 )

@@ -355,10 +355,19 @@ int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t ma
  *     rt_render_device then returns once every run has been rendered (the
  *     claims follow the devices' progress); the frame is bit-identical to
  *     the static split's and to one device's.  rt_last_dealing reports the
- *     split.                                                             */
+ *     split.
+ *   RT_OPT_TAIL: the long tail of deep renders without lights (MaxDepth >
+ *     8; RandomScene, HDRITestScene): once at most a threshold of paths is
+ *     left, one persistent launch carries each of them through all its
+ *     remaining bounces (closest hit and shading in one lane) instead of
+ *     two launches per bounce.  Same operations per path in the same order:
+ *     the frame is bit-identical.  0 (default) = automatic (2^20 paths), 1 =
+ *     off (every bounce through the per-bounce kernels), n > 1 = threshold
+ *     of n paths.                                                        */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7,
-       RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9, RT_OPT_DEALING = 10, RT_OPT_DEAL_FIRST = 11 };
+       RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9, RT_OPT_DEALING = 10, RT_OPT_DEAL_FIRST = 11,
+       RT_OPT_TAIL = 12 };
 enum { RT_DEAL_STATIC = 0, RT_DEAL_DYNAMIC = 1 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1, RT_NODES_WIDE8 = 2 };

@@ -169,3 +169,26 @@ def test_wavefront_kernels_wide8_nodes_match_oracle(wave, O, g, tmp_path, name, 
     ref = O.render(s.desc, cam, g.make_params(spp, cam.max_depth, seed=seed), fp32=True)
     got = np.fromfile(out, np.float32).reshape(ref.shape)
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-5), float(np.abs(got - ref).max())
+
+
+@pytest.mark.parametrize("name,tail_after,nodes", [("random", 0, "0"), ("random", 7, "0"), ("hdri-test", 2, "0"),
+                                                   ("random", 3, "2"), ("simple", 1, "0")])
+def test_tail_kernel_bit_identical(wave, tmp_path, name, tail_after, nodes):
+    """The long-tail kernel (k_tail: one lane carries a path through all its
+    remaining bounces, trav_step then shade_path) under ASan/UBSan: handed
+    the paths left after bounce `tail_after`, the frame equals the one the
+    per-bounce kernels render, bit for bit (RT_OPT_TAIL's claim)."""
+    spp, seed, width = 2, 5, 48
+    outs = {}
+    for mode in ("wave", "tail"):
+        out = tmp_path / f"{name}_{mode}.f32"
+        env = _env()
+        env["RTG_EMU_QUANT"] = nodes
+        if mode == "tail":
+            env["RTG_EMU_TAIL"] = str(tail_after)
+        r = subprocess.run([wave, name, str(width), str(spp), str(seed), ASSETS, str(out)], capture_output=True,
+                           text=True, env=env, timeout=600)
+        assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+        outs[mode] = np.fromfile(out, np.float32)
+    assert outs["wave"].sum() > 0
+    assert np.array_equal(outs["wave"], outs["tail"])

@@ -202,3 +202,36 @@ def test_collapse_option_same_frame(g, ctx, name):
     assert nodes[g.RT_COLLAPSE_SAH] <= nodes[g.RT_COLLAPSE_GREEDY]
     assert np.isfinite(frames[g.RT_COLLAPSE_SAH]).all()
     assert np.array_equal(frames[g.RT_COLLAPSE_GREEDY], frames[g.RT_COLLAPSE_SAH])
+
+
+@pytest.mark.parametrize("name,kw,nodes", [("random", dict(width=160), "fp32"), ("hdri-test", dict(width=160), "fp32"),
+                                           ("random", dict(width=160), "wide8"),
+                                           ("cornell", dict(width=64), "fp32")])
+def test_tail_kernel_same_frame(g, name, kw, nodes):
+    """RT_OPT_TAIL: the long-tail kernel (k_tail) that carries the last paths
+    of a deep render without lights to their ends renders the same frame, bit
+    for bit, as every bounce through the per-bounce kernels, at every hand-off
+    size (2 = almost never, 2^30 = at the first check) and with both twin
+    counts; a scene with lights (cornell) never hands off.  Negative values
+    are refused."""
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    p = g.make_params(16, cam.max_depth, seed=7)
+    c = g.Context(0)
+    try:
+        with pytest.raises(g.RTError):
+            c.set_option(g.RT_OPT_TAIL, -1)
+        c.set_node_format(nodes)
+        c.upload(s.desc)
+        frames = {}
+        for tail in (1, 2, 1 << 14, 1 << 30):
+            for streams in (1, 2):
+                c.set_tail(tail)
+                c.set_schedule(streams=streams)
+                frames[tail, streams], _ = c.render(cam, p)
+        ref = frames[1, 1]
+        assert np.isfinite(ref).all() and ref.sum() > 0
+        for k, f in frames.items():
+            assert np.array_equal(f, ref), k
+    finally:
+        c.close()

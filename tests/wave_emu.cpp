@@ -31,6 +31,7 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
   uint32_t* fetch_ext = a.counts + CNT_FETCH_EXT;
   uint32_t* fetch_sh = a.counts + CNT_FETCH_SH;
   for (double* p = a.acc; p < a.acc + size_t(a.npix) * 3; ++p) *p = 0.0;
+  const int tail_after = getenv("RTG_EMU_TAIL") ? atoi(getenv("RTG_EMU_TAIL")) : -1;
   for (uint32_t s0 = 0; s0 < spp; s0 += spb) {
     const uint32_t sb = spp - s0 < spb ? spp - s0 : spb;
     const uint32_t nslots = sb * a.npix;
@@ -49,6 +50,12 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
       if (sc.num_lights > 0) {   // as run_batches: no lights, no NEE launches
         k_shadow<kRing, false, kVol, kEnvIS, kQuant, kWide>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
         k_nee_apply<kEnvIS>(a, cnt_shadow);
+      }
+      // RTG_EMU_TAIL=b: after bounce b the long-tail kernel carries every
+      // path left to its end (run_batches' hand-off, scenes without lights)
+      if (sc.num_lights == 0 && tail_after >= 0 && b == tail_after && b + 1 < max_depth) {
+        k_tail<kRing, kVol, kShade, kQuant, kWide>(sc, cam, a, a.s[nx], cnt_stream[nx], fetch_ext);
+        break;
       }
     }
     k_accum(a, sb);
