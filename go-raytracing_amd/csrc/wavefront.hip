@@ -956,8 +956,10 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
     const uint32_t kk = GIX(k, a.slots, 59);
-    const uint32_t flags = ldnt(&a.sj_info[kk]) & 0xFFu, vis = ldnt(&a.sj_vis[kk]);
-    if ((flags & vis & 3u) == 0u) continue;
+    // (k_shadow sets a visibility bit only for a ray the job asked for, so
+    // the job's flag word need not be read: vis & flags == vis)
+    const uint32_t vis = ldnt(&a.sj_vis[kk]);
+    if ((vis & 3u) == 0u) continue;
     const float4 ea = ldnt(&a.ne_a[kk]);
     float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
     const float4 L4 = ldnt(Lp);
@@ -965,8 +967,8 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
     if (kEnvIS) {
       const float4 pb = ldnt(&a.ne_beta[kk]);
       V3 direct = mk(0.0f, 0.0f, 0.0f);
-      if ((flags & 2u) && (vis & 2u)) { const float4 eh = ldnt(&a.ne_h[kk]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
-      if ((flags & 1u) && (vis & 1u)) direct = add(direct, mk(ea.x, ea.y, ea.z));
+      if (vis & 2u) { const float4 eh = ldnt(&a.ne_h[kk]); direct = add(direct, mk(eh.x, eh.y, eh.z)); }
+      if (vis & 1u) direct = add(direct, mk(ea.x, ea.y, ea.z));
       L = add(mk(L4.x, L4.y, L4.z), mul(mk(pb.x, pb.y, pb.z), direct));
     } else {
       L = add(mk(L4.x, L4.y, L4.z), mk(ea.x, ea.y, ea.z));
