@@ -461,6 +461,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     a.spill = static_cast<uint32_t*>(ctx->wspill.p) + size_t(t) * spill_words;
     a.slots = uint32_t(S);
     a.out_pixels = uint32_t(dc.width) * uint32_t(dc.height);
+    a.keep_vis = ctx->probing ? 1 : 0;
     ctx->twin_args[t] = a;
   }
   // the twins' slices must lie inside the batch buffers (an internal error

@@ -51,6 +51,7 @@ struct WaveArgs {
   int32_t spill_cap;
   uint32_t slots;   // capacity of every per-slot array (RTG_GUARD bounds checks)
   uint32_t out_pixels;  // pixels of the output frame (RTG_GUARD: k_finalize's scattered store)
+  int32_t keep_vis;     // k_shadow stores the visibility words even when it applies the NEE itself (path probes)
 };
 
 // Queue counters, each on its own 128-B line (same-line atomics serialise);

@@ -159,6 +159,15 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 #ifndef RTG_TAIL_GRID
 #define RTG_TAIL_GRID 1
 #endif
+// NEE contributions added by k_shadow with no-return float atomics (scenes
+// without HDRI importance sampling): no k_nee_apply launch.  Bit-identical
+// frames, but measured much slower (C4 2029 -> 1811 Msamples/s, k_shadow
+// 52.4 -> 89.9 ms per frame against k_nee_apply's 11.7: three scattered
+// float atomics per visible job, each a line fetched into L2 and modified
+// there, plus 35 VGPRs spilled at the 72 cap); a diagnostic variant
+#ifndef RTG_NEE_ATOMIC
+#define RTG_NEE_ATOMIC 0
+#endif
 constexpr uint32_t kSegs = 8;
 constexpr uint32_t kSegStride = 32;   // words between the segment counters
 struct Pool {
@@ -861,6 +870,10 @@ __global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamer
 template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kQuant = false, bool kWide = false>
 __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
                                                                 uint32_t* fetch, uint32_t* zero_c) {
+  // RTG_NEE_ATOMIC: without HDRI importance sampling (an area-light ray per
+  // job) the visible contribution is added to Lout here and no k_nee_apply
+  // runs (run_batches)
+  constexpr bool kNeeAtomic = RTG_NEE_ATOMIC && !kEnvIS;
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
   if (blockIdx.x == 0 && threadIdx.x == 0)   // next extend's segment counters
     for (uint32_t k = 0; k < kSegs; ++k) zero_c[k * kSegStride] = 0u;
@@ -882,6 +895,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   float4 da = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   // prefetched job
   float4 qp = da, qa = da, qh = da;
+  float4 qe = da;   // kNeeAtomic: the job's contribution (x beta) and path slot (ne_a)
   uint32_t qinfo = 1u;
   auto start_ray = [&](int rr, V3 dir, float tmax) -> int {
     if (kCount) cnt.shadow++;
@@ -899,7 +913,21 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       if (s2 == TRAV_RUNNING) return false;
       if (s2 != TRAV_ANYHIT) vis |= 1u;
     }
-    stnt(&a.sj_vis[p], vis);
+    // (the words k_nee_apply reads; with kNeeAtomic only the path probe
+    // reads them: a 4-B scattered store per job saved)
+    if (!kNeeAtomic || a.keep_vis) stnt(&a.sj_vis[p], vis);
+    if (kNeeAtomic && (vis & 1u)) {
+      // k_nee_apply's L + contribution, here: one float add per component in
+      // the L2 atomic unit, with no return (the lane does not wait).  Within
+      // a bounce this is the only update of Lout[slot] (one NEE job per
+      // path; k_shade's adds are in the kernels before and after), so the
+      // sum is k_nee_apply's, bit for bit.  da holds ne_a once the job's
+      // area ray has started (see the job start below).
+      float* Lp = &a.Lout[GIX(asu(da.w), a.slots, 47)].x;
+      atomicAddNoRet(Lp, da.x);
+      atomicAddNoRet(Lp + 1, da.y);
+      atomicAddNoRet(Lp + 2, da.z);
+    }
     return true;
   };
   for (;;) {
@@ -919,6 +947,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
         r = 1;
         s = start_ray(1, mk(da.x, da.y, da.z), da.w);               // camera.go:639
       }
+      if (kNeeAtomic) da = qe;   // the area direction is dead once its ray started (no HDRI ray follows)
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE && (p == ITEM_NONE || !Q.tail), Q, fetch, n, nwaves, a.refill);
@@ -928,6 +957,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       qa = ldnt(&a.sj_a[pn]);
       if (kEnvIS) qh = ldnt(&a.sj_h[pn]);
       if (kEnvIS || kVol) qinfo = ldnt(&a.sj_info[pn]);
+      if (kNeeAtomic) qe = ldnt(&a.ne_a[pn]);
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (Q.dry) break;
@@ -1143,8 +1173,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
                              cnt_shadow, fetch_sh, fetch_ext);
           if ((e = mark_end(plan, st)) != hipSuccess) return e;
           RTG_LAUNCHED("k_shadow", b, st);
-          hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap[t]), dim3(256), 0, st, a, cnt_shadow);
-          RTG_LAUNCHED("k_nee_apply", b, st);
+          if (kEnvIS || !RTG_NEE_ATOMIC) {   // (else k_shadow applied the contributions)
+            hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap[t]), dim3(256), 0, st, a, cnt_shadow);
+            RTG_LAUNCHED("k_nee_apply", b, st);
+          }
         }
       }
       if (plan.max_depth > 8 && ((b >= 7 && (b % 4) == 3) || (plan.tail_rays > 0 && b == plan.tail_first))) {

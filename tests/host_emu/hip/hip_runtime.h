@@ -48,6 +48,7 @@ inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return v; }
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 inline int __ffsll(unsigned long long x) { return __builtin_ffsll(static_cast<long long>(x)); }
 inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { const uint32_t o = *p; *p = o + v; return o; }
+inline void atomicAddNoRet(float* p, float v) { *p = *p + v; }   // one lane: the plain add
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   const unsigned long long o = *p; *p = o + v; return o;
 }

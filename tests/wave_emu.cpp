@@ -49,7 +49,7 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
       }
       if (sc.num_lights > 0) {   // as run_batches: no lights, no NEE launches
         k_shadow<kRing, false, kVol, kEnvIS, kQuant, kWide>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
-        k_nee_apply<kEnvIS>(a, cnt_shadow);
+        if (kEnvIS || !RTG_NEE_ATOMIC) k_nee_apply<kEnvIS>(a, cnt_shadow);   // as run_batches
       }
       // RTG_EMU_TAIL=b: after bounce b the long-tail kernel carries every
       // path left to its end (run_batches' hand-off, scenes without lights)
@@ -112,6 +112,7 @@ int main(int argc, char** argv) {
   a.spill_cap = kStackMax - kRing;
   a.slots = uint32_t(S);
   a.out_pixels = uint32_t(npix);
+  a.keep_vis = 1;
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
   const bool vol = d.has_volumes != 0 || d.n_circles > 0 || d.dfs_order != 0, envis = d.env.valid && d.env.use_is;
