@@ -994,7 +994,7 @@ static int device_builds(rt_ctx* ctx) {
                           ctx->stream));
   }
   h.stack_needed = (h.tlas_need4 + h.max_leaf_inst + 1 + need + 2) * (h.dfs_order ? 2 : 1);
-  if (h.stack_needed > 64)   // the BVH4 bound (the probe kernels' LDS stack)
+  if (h.stack_needed > kStackMax)
     return set_err(ctx, RT_ERR_UNSUPPORTED, "device-built BVH too deep for the traversal stack");
   d.stack_needed = h.stack_needed;
   d.n_nodes = tgt.nodes_used;
@@ -1447,7 +1447,7 @@ int rt_primary_hits(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32
   int* perr = static_cast<int*>(ctx->errflag.p) + 1;   // the probe's own flag word
   HIPCHK(hipMemsetAsync(perr, 0, sizeof(int), ctx->stream));
   HIPCHK(launch_primary(ctx->dscene, dc, seed, sample, top, prim, t, perr,
-                        ctx->host.stack_needed <= 32 ? 32 : 64, ctx->stream));
+                        ctx->host.stack_needed <= 32 ? 32 : ctx->host.stack_needed <= 64 ? 64 : 128, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_prim, prim, n * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(out_t, t, n * 4, hipMemcpyDeviceToHost, ctx->stream));

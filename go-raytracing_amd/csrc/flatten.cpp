@@ -734,6 +734,20 @@ struct Flattener {
   int max_leaf_inst = 0;
 
   // World BVH node -> item, refit box (planes excluded).
+  // A RotateX / RotateZ anywhere in the object graph below g
+  bool under_rot_xz(int g, int depth) {
+    if (!valid_index(g) || depth > 200) return false;
+    const rt_hittable& h = H(g);
+    if (h.kind == RT_ROTATE_X || h.kind == RT_ROTATE_Z) return true;
+    if (is_wrapper(h.kind) || h.kind == RT_VOLUME) return under_rot_xz(h.a, depth + 1);
+    if (h.kind == RT_BVH_NODE) return under_rot_xz(h.a, depth + 1) || (h.b != h.a && under_rot_xz(h.b, depth + 1));
+    if (h.kind == RT_LIST || h.kind == RT_BVH_LEAF) {
+      for (int c : children_of(h))
+        if (under_rot_xz(c, depth + 1)) return true;
+    }
+    return false;
+  }
+
   uint32_t tlas_item(int g, int depth, Box& box) {
     if (depth > 200) { fail(RT_ERR_UNSUPPORTED, "world BVH too deep"); return empty_leaf; }
     if (depth > S.tlas_depth) S.tlas_depth = depth;
@@ -751,13 +765,18 @@ struct Flattener {
       Box lb, rb;
       uint32_t li = tlas_item(h.a, depth + 1, lb);
       uint32_t ri = tlas_item(h.b, depth + 1, rb);
-      DNode& n = S.nodes[idx];
-      store_box(n.l, lb);
-      store_box(n.r, rb);
-      n.litem = lb.empty() ? empty_leaf : li;
-      n.ritem = rb.empty() ? empty_leaf : ri;
       box.merge(lb);
       box.merge(rb);
+      // BVHNode.Hit (bvh.go:219-239) tests only its own bbox, never a
+      // child's: a child that is not a BVH node is reached whenever this
+      // node is.  A slot box only matters where the child's Hit can report
+      // hits outside its bbox (a RotateX / RotateZ below it): such a slot
+      // gets this node's box, which the reference did test
+      DNode& n = S.nodes[idx];
+      store_box(n.l, H(h.a).kind != RT_BVH_NODE && under_rot_xz(h.a, 0) ? box : lb);
+      store_box(n.r, H(h.b).kind != RT_BVH_NODE && under_rot_xz(h.b, 0) ? box : rb);
+      n.litem = lb.empty() ? empty_leaf : li;
+      n.ritem = rb.empty() ? empty_leaf : ri;
       return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
     }
     if (h.kind == RT_BVH_LEAF || h.kind == RT_LIST) return tlas_leaf(children_of(h), 1, box);
@@ -1528,7 +1547,10 @@ struct Flattener {
     // entry's box entry distance beside it: twice the words
     S.dfs_order = tlas_sah_ok() ? 0 : 1;
     if (S.dfs_order) S.stack_needed *= 2;
-    if (S.stack_needed > 64) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
+    // 128 entries: the wavefront kernels' LDS ring + global spill
+    // (wavefront.h kStackMax) and the probe's largest LDS stack; RotateX/Z
+    // scenes take two words per entry, so their BVHs may be half as deep
+    if (S.stack_needed > 128) fail(RT_ERR_UNSUPPORTED, "BVH too deep for the device traversal stack");
     // RT_NODES_WIDE8: only for scenes the 8-wide traversal runs (not the
     // rare-primitive variant: no reference-order mode, no circles, no volume
     // left in the world BVH) and whose BLASes are all built here

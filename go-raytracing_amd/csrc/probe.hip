@@ -182,9 +182,12 @@ hipError_t launch_primary(const DScene& sc, const DCamera& cam, uint32_t seed, i
   if (stack <= 32) {
     if (q) hipLaunchKernelGGL((primary_kernel<32, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
     else hipLaunchKernelGGL((primary_kernel<32, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
-  } else {
+  } else if (stack <= 64) {
     if (q) hipLaunchKernelGGL((primary_kernel<64, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
     else hipLaunchKernelGGL((primary_kernel<64, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+  } else {   // deep scenes (RotateX / RotateZ chains: two words per entry), 145 KB of LDS per block
+    if (q) hipLaunchKernelGGL((primary_kernel<128, true>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
+    else hipLaunchKernelGGL((primary_kernel<128, false>), grid, block, 0, st, sc, cam, seed, sample, top, prim, t, err);
   }
   return hipGetLastError();
 }

@@ -42,10 +42,10 @@ enum rt_status {
   RT_ERR_UNSUPPORTED = -2, /* Go type or nesting the GPU path does not take;
                               the caller falls back to rt.BucketRenderer.
                               Includes a BVH whose worst traversal needs more
-                              than 64 stack entries; a scene holding a
+                              than 128 stack entries; a scene holding a
                               RotateX / RotateZ wrapper traverses in the
                               reference's DFS order with two words per entry
-                              (DESIGN.md §3), so its limit is 32 entries    */
+                              (DESIGN.md §3), so its limit is 64 entries    */
   RT_ERR_HIP = -3,         /* HIP runtime error (message in rt_last_error)  */
   RT_ERR_OOM = -4,         /* device allocation failed                      */
   RT_ERR_NO_SCENE = -5,    /* rt_render before rt_scene_upload              */

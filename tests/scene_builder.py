@@ -116,6 +116,21 @@ class Builder:
         bb = [nx.min(), nx.max(), pts[:, 1].min(), pts[:, 1].max(), nz.min(), nz.max()]
         return self._add(self.g.RT_ROTATE_Y, -1, child, 0, self._pad(bb), [sin_t, cos_t])
 
+    def rotate_x(self, child, sin_t, cos_t):
+        """RotateX (transform.go:201-237): bbox = the child's corners rotated about x."""
+        b = self.h[child].bbox
+        pts = np.array([[x, y, z] for x in b[0:2] for y in b[2:4] for z in b[4:6]], float)
+        ny = cos_t * pts[:, 1] - sin_t * pts[:, 2]
+        nz = sin_t * pts[:, 1] + cos_t * pts[:, 2]
+        bb = [pts[:, 0].min(), pts[:, 0].max(), ny.min(), ny.max(), nz.min(), nz.max()]
+        return self._add(self.g.RT_ROTATE_X, -1, child, 0, self._pad(bb), [sin_t, cos_t])
+
+    def bvh_node(self, left, right):
+        """BVHNode{left, right} (bvh.go): bbox = the union of the children's."""
+        l, r = self.h[left].bbox, self.h[right].bbox
+        bb = [min(l[0], r[0]), max(l[1], r[1]), min(l[2], r[2]), max(l[3], r[3]), min(l[4], r[4]), max(l[5], r[5])]
+        return self._add(self.g.RT_BVH_NODE, -1, left, right, bb, [])
+
     def scale(self, child, f):
         """Scale (transform.go:360-403): bbox corners times the factor."""
         b = self.h[child].bbox
