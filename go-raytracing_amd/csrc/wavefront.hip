@@ -21,6 +21,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#ifdef RTG_WAVETIME
+#include <algorithm>
+#include <vector>
+#endif
 
 #include "dev_layout.h"
 #include "device_common.h"
@@ -247,10 +251,32 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   return idx;
 }
 
+#ifdef RTG_WAVETIME
+// Diagnostic builds only: per wave of the last traversal launch, its start
+// and end on the 100 MHz wall clock and the rays it traced (run_batches
+// prints the distribution after each launch).  Vector stores from lane 0.
+constexpr int kWtWaves = 16384;
+__device__ unsigned long long rtg_wt[3 * kWtWaves];
+__device__ __forceinline__ void wavetime_note(unsigned long long t0, uint32_t rays) {
+  const unsigned long long t1 = wall_clock64();
+  for (int o = 32; o > 0; o >>= 1) rays += __shfl_xor(rays, o);
+  const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (__lane_id() == 0 && w < uint32_t(kWtWaves)) {
+    rtg_wt[3 * w] = t0;
+    rtg_wt[3 * w + 1] = t1;
+    rtg_wt[3 * w + 2] = rays;
+  }
+}
+#endif
+
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
   const float4 r = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
                                asf(uint32_t(b.refpos)));
+#ifdef RTG_DIAG_NO_RESULT_STORES
+  // diagnostic bound only (wrong frames): the store kept but never taken
+  if (__float_as_uint(r.x) == 0x7FC00123u)
+#endif
   stnt(&hit[p], r);
 }
 
@@ -289,11 +315,18 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   float4 po = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pd = po;
   uint32_t pb = 0;
+#ifdef RTG_WAVETIME
+  const unsigned long long wt0 = wall_clock64();
+  uint32_t wt_rays = 0;
+#endif
   for (;;) {
     if (p == ITEM_NONE && pn != ITEM_NONE) {
       p = pn;
       pn = ITEM_NONE;
       if (kCount) cnt.rays++;
+#ifdef RTG_WAVETIME
+      wt_rays++;
+#endif
       if (kFirst) {
         V3 ro, rd;
         uint32_t key;
@@ -325,6 +358,9 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
   }
+#ifdef RTG_WAVETIME
+  wavetime_note(wt0, wt_rays);
+#endif
 #ifdef RTG_STAMP
   add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
 #else
@@ -915,6 +951,9 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
     }
     // (the words k_nee_apply reads; with kNeeAtomic only the path probe
     // reads them: a 4-B scattered store per job saved)
+#ifdef RTG_DIAG_NO_RESULT_STORES
+    if (vis == 0xDEADu)
+#endif
     if (!kNeeAtomic || a.keep_vis) stnt(&a.sj_vis[p], vis);
     if (kNeeAtomic && (vis & 1u)) {
       // k_nee_apply's L + contribution, here: one float add per component in
@@ -1089,6 +1128,36 @@ static hipError_t mark_end(const WavePlan& plan, hipStream_t st) {
     }                                                                                                  \
   } while (0)
 
+#ifdef RTG_WAVETIME
+// After a traversal launch (diagnostic builds): the waves' end times after
+// the first start, as percentiles, the last start, and the rays per wave.
+static hipError_t wavetime_report(const char* name, int bounce, int nwaves, hipStream_t st) {
+  hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return e;
+  if (nwaves > kWtWaves) nwaves = kWtWaves;
+  std::vector<unsigned long long> h(size_t(3) * nwaves);
+  if ((e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rtg_wt), h.size() * sizeof(unsigned long long))) != hipSuccess) return e;
+  unsigned long long t0 = ~0ull, s_last = 0;
+  for (int w = 0; w < nwaves; ++w) t0 = std::min(t0, h[3 * w]);
+  std::vector<double> ends(nwaves), rays(nwaves);
+  double tot = 0;
+  for (int w = 0; w < nwaves; ++w) {
+    ends[w] = double(h[3 * w + 1] - t0) / 100.0;   // us
+    s_last = std::max(s_last, h[3 * w] - t0);
+    rays[w] = double(h[3 * w + 2]);
+    tot += rays[w];
+  }
+  std::vector<double> se = ends, sr = rays;
+  std::sort(se.begin(), se.end());
+  std::sort(sr.begin(), sr.end());
+  auto pc = [&](const std::vector<double>& v, double q) { return v[size_t(q * (v.size() - 1))]; };
+  fprintf(stderr, "RTG_WAVETIME %s b%d waves %d rays %.0f | last start %.1f us | end p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us | rays/wave p10 %.0f p50 %.0f p99 %.0f\n",
+          name, bounce, nwaves, tot, double(s_last) / 100.0, pc(se, 0.1), pc(se, 0.5), pc(se, 0.9), pc(se, 0.99), se.back(),
+          pc(sr, 0.1), pc(sr, 0.5), pc(sr, 0.99));
+  return hipSuccess;
+}
+#endif
+
 // The render's work is split into twins (WavePlan::num_twins, 1 or 2):
 // disjoint halves of the pixel list, each with its own path slots, queue
 // counters, spill area and HIP stream, enqueued bounce by bounce in
@@ -1155,6 +1224,9 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         if (offset && t == 0 && (e = hipEventRecord(plan.offset_ev, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_extend", b, st);
+#ifdef RTG_WAVETIME
+        if ((e = wavetime_report("k_extend", b, b == 0 ? gext0[t] * 4 : gext[t] * 4, st)) != hipSuccess) return e;
+#endif
         if ((e = mark_begin(plan, uint8_t(KC_SHADE | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, true>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
