@@ -1155,6 +1155,16 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
 #endif
     }
     if (kCount) cnt.nodes++;
+#ifdef RTG_EXTRA_VALU   // diagnostic: RTG_EXTRA_VALU more VALU per node step (four independent chains)
+    {
+      float x0 = t0, x1 = t1, x2 = t2, x3 = t3;
+      for (int k = 0; k < RTG_EXTRA_VALU / 4; ++k) {
+        x0 = fmaf(x0, 1.0001f, 0.5f); x1 = fmaf(x1, 1.0001f, 0.5f);
+        x2 = fmaf(x2, 1.0001f, 0.5f); x3 = fmaf(x3, 1.0001f, 0.5f);
+      }
+      asm volatile("" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3));
+    }
+#endif
 #ifdef RTG_STAMP
     const uint32_t st1 = rtg_stamp();
 #endif
