@@ -696,7 +696,11 @@ constexpr uint32_t ITEM_POP = 0xFFFFFFFEu;   // "take the next item from the sta
 // spill column is spill_blk + (its LDS slot - lds0), formed on the rare
 // spill path, the ray words sit at lds + cap * stride and the hit record
 // after them.
-constexpr int kWorldRayWords = 11;  // LDS words per lane: world ray (9), time, current instance ref
+// LDS words per lane: world ray origin and direction (6), time, current
+// instance ref; + its 1/d (3) when TStack::winv, else recomputed on instance
+// exit (make_tray, bit for bit: three IEEE divides on the exit path)
+constexpr int kWorldRayWords = 8;
+constexpr int kWorldInvWords = 3;
 constexpr int kHitWords = 3;        // LDS words per lane: hit record (closest-hit kernels)
 struct TStack {
   uint32_t* lds;       // this lane's slot 0
@@ -706,6 +710,8 @@ struct TStack {
   const uint32_t* lds0;  // the block's slot-0 row (lane = lds - lds0)
   int sstride;         // words between spill entries
   int spill_cap;
+  const float4* ln = nullptr;   // the block's LDS copy of BVH4 nodes [0, kLdsNodes) (trav_step)
+  bool winv = false;            // the world ray's 1/d is kept in LDS (kWorldInvWords more per lane)
   __device__ __forceinline__ float* wrp() const { return reinterpret_cast<float*>(lds + cap * stride); }
   __device__ __forceinline__ uint32_t* spill_at(int k) const {
     return spill_blk + (lds - lds0) + size_t(GIX(k, spill_cap, 25)) * sstride;
@@ -714,22 +720,28 @@ struct TStack {
     float* wr = wrp();
     wr[0] = o.x; wr[stride] = o.y; wr[2 * stride] = o.z;
     wr[3 * stride] = d.x; wr[4 * stride] = d.y; wr[5 * stride] = d.z;
-    wr[6 * stride] = inv.x; wr[7 * stride] = inv.y; wr[8 * stride] = inv.z;
+    if (winv) { wr[8 * stride] = inv.x; wr[9 * stride] = inv.y; wr[10 * stride] = inv.z; }
+  }
+  // the world ray back (leaving an instance)
+  __device__ __forceinline__ TRay world_ray() const {
+    const float* wr = wrp();
+    const V3 o = mk(wr[0], wr[stride], wr[2 * stride]), d = mk(wr[3 * stride], wr[4 * stride], wr[5 * stride]);
+    if (!winv) return make_tray(o, d);
+    TRay r; r.o = o; r.d = d; r.inv = mk(wr[8 * stride], wr[9 * stride], wr[10 * stride]);
+    return r;
   }
   __device__ __forceinline__ V3 wo() const { const float* wr = wrp(); return mk(wr[0], wr[stride], wr[2 * stride]); }
   __device__ __forceinline__ V3 wd() const {
     const float* wr = wrp();
     return mk(wr[3 * stride], wr[4 * stride], wr[5 * stride]);
   }
-  __device__ __forceinline__ V3 winv() const {
-    const float* wr = wrp();
-    return mk(wr[6 * stride], wr[7 * stride], wr[8 * stride]);
+  __device__ __forceinline__ float time() const { return wrp()[6 * stride]; }
+  __device__ __forceinline__ void set_time(float t) const { wrp()[6 * stride] = t; }
+  __device__ __forceinline__ int cur_ref() const { return reinterpret_cast<const int*>(wrp())[7 * stride]; }
+  __device__ __forceinline__ void set_cur_ref(int r) const { reinterpret_cast<int*>(wrp())[7 * stride] = r; }
+  __device__ __forceinline__ int* hitp() const {
+    return reinterpret_cast<int*>(lds + (cap + kWorldRayWords + (winv ? kWorldInvWords : 0)) * stride);
   }
-  __device__ __forceinline__ float time() const { return wrp()[9 * stride]; }
-  __device__ __forceinline__ void set_time(float t) const { wrp()[9 * stride] = t; }
-  __device__ __forceinline__ int cur_ref() const { return reinterpret_cast<const int*>(wrp())[10 * stride]; }
-  __device__ __forceinline__ void set_cur_ref(int r) const { reinterpret_cast<int*>(wrp())[10 * stride] = r; }
-  __device__ __forceinline__ int* hitp() const { return reinterpret_cast<int*>(lds + (cap + kWorldRayWords) * stride); }
   __device__ __forceinline__ void set_hit(int kind, int idx, int refpos, int primpos) const {
     int* h = hitp();
     h[0] = int((uint32_t(kind) << 28) | (uint32_t(idx) & 0x0FFFFFFFu)); h[stride] = refpos; h[2 * stride] = primpos;
@@ -764,10 +776,21 @@ struct TStack {
     return v;
   }
 };
-// LDS words per lane: `cap` stack entries + the 9-float world ray (+ the
-// 4-word hit record for closest-hit traversal).
+// LDS words per lane: `cap` stack entries + the 8-word world ray (+ the
+// 3-word hit record for closest-hit traversal).
 __device__ __forceinline__ TStack lds_stack_only(uint32_t* lds, int stride, int cap) {
   return TStack{lds, stride, cap, nullptr, lds, 0, 0};
+}
+// The block's LDS copy of BVH4 nodes [0, K) (trav_step kLdsN = K): called by
+// every thread of the block before its first traversal step.
+template <int K>
+__device__ __forceinline__ void lds_nodes_fill(const DScene& sc, float4* ln) {
+  if constexpr (K > 0) {
+    const uint32_t nn = (sc.n_nodes < uint32_t(K) ? sc.n_nodes : uint32_t(K)) * 8u;
+    const float4* const src = reinterpret_cast<const float4*>(sc.nodes);
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) ln[i] = src[i];
+    __syncthreads();
+  }
 }
 
 // Resumable traversal state (one lane, one ray).
@@ -818,6 +841,14 @@ constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackV
 #define RTG_P2_SLACK 0
 #endif
 constexpr int kP2Slack = RTG_P2_SLACK;
+// The LDS node cache read through flat loads (one code path; A/B knob)
+#ifndef RTG_LDS_FLAT
+#define RTG_LDS_FLAT 0
+#endif
+// Phase 2's record gather loads only the rows the lane's record uses (A/B knob)
+#ifndef RTG_GATHER_TRIM
+#define RTG_GATHER_TRIM 0
+#endif
 // BVH4 fp32 slab arithmetic in packed fp32 (v_pk_add_f32 / v_pk_mul_f32):
 // half the slab VALU instructions, bit-identical, but measured slower (C4
 // 2018 -> 1934 Msamples/s, k_extend 99.5 -> 107 ms per frame: 13 VGPRs
@@ -930,7 +961,10 @@ __device__ __forceinline__ int trav_init(const DScene& sc, Trav& T, const TStack
 //   kAny = false: closest hit in [tmin, tmax) with the tie rule.
 //   kAny = true : any hit in [tmin, tmax] (shadow rays, camera.go:582,639).
 //   kQuant = true: the node records are DNodeQ (RT_NODES_QUANT8), else DNode4.
-template <bool kAny, bool kCount, bool kVol, bool kQuant = false, bool kWide = false>
+//   kLdsN > 0: BVH4 nodes [0, kLdsN) are read from the block's LDS copy S.ln
+//   (lds_nodes_fill; flatten puts the world BVH and the BLASes' top levels
+//   first), the others from global memory.
+template <bool kAny, bool kCount, bool kVol, bool kQuant = false, bool kWide = false, int kLdsN = 0>
 __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack& S, Cnt& cnt, int* err) {
   // Reference-order mode (DScene.dfs_order; only in the rare-primitive kVol
   // variant, closest hit): scenes holding a RotateX / RotateZ wrapper, whose
@@ -1108,18 +1142,38 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       // far plane of each axis is picked by the load address (the
       // direction's signs) instead of per-child selects: box_hit, bit for bit.
       const uint32_t nb = nidx << 7;
-      const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
-      auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };
       const uint32_t sxo = (__float_as_uint(T.cr.inv.x) >> 27) & 16u, syo = (__float_as_uint(T.cr.inv.y) >> 27) & 16u,
                      szo = (__float_as_uint(T.cr.inv.z) >> 27) & 16u;
-      const float4 nx = ldn(nb + sxo), fx = ldn(nb + (16u - sxo)), ny = ldn(nb + (32u + syo)), fy = ldn(nb + (48u - syo));
-      const float4 nz = ldn(nb + (64u + szo)), fz = ldn(nb + (80u - szo));
-      it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
+      float4 nx, fx, ny, fy, nz, fz;
+      if (RTG_LDS_FLAT && kLdsN > 0) {
+        // one flat-load path: the lane's node base in LDS or in global memory
+        const char* const fbase = nidx < uint32_t(kLdsN) ? reinterpret_cast<const char*>(S.ln)
+                                                         : reinterpret_cast<const char*>(sc.nodes);
+        auto ldf = [&](uint32_t off) { return *reinterpret_cast<const float4*>(fbase + off); };
+        nx = ldf(nb + sxo); fx = ldf(nb + (16u - sxo)); ny = ldf(nb + (32u + syo)); fy = ldf(nb + (48u - syo));
+        nz = ldf(nb + (64u + szo)); fz = ldf(nb + (80u - szo));
+        it = *reinterpret_cast<const uint4*>(fbase + (nb + 96u));
+      } else if (kLdsN > 0 && nidx < uint32_t(kLdsN)) {
+        // the hot nodes from LDS: off the vector-memory path (TA / TD) that
+        // the global node fetches saturate
+        const char* const lbase = reinterpret_cast<const char*>(S.ln);
+        auto ldl = [&](uint32_t off) { return *reinterpret_cast<const float4*>(lbase + off); };
+        nx = ldl(nb + sxo); fx = ldl(nb + (16u - sxo)); ny = ldl(nb + (32u + syo)); fy = ldl(nb + (48u - syo));
+        nz = ldl(nb + (64u + szo)); fz = ldl(nb + (80u - szo));
+        it = *reinterpret_cast<const uint4*>(lbase + (nb + 96u));
+      } else {
+        const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
+        auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };
+        nx = ldn(nb + sxo); fx = ldn(nb + (16u - sxo)); ny = ldn(nb + (32u + syo)); fy = ldn(nb + (48u - syo));
+        nz = ldn(nb + (64u + szo)); fz = ldn(nb + (80u - szo));
+        it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
 #if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
-      asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));   // as above
+        asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));   // as above
 #endif
+      }
 #ifdef RTG_EXTRA_LOAD   // diagnostic: one more 16-B load per node step (the node's unused last row)
-      { const float4 x = ldn(nb + 112u); asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w)); }
+      { const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.nodes) + nb + 112u);
+        asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w)); }
 #endif
 #ifdef RTG_STAMP
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1201,7 +1255,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     }   // BVH4 node
     // leaving an instance with nothing postponed: restore the world ray inline
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END && T.lf == ITEM_NONE) {
-      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
+      T.cr = S.world_ray(); S.set_cur_ref(-1);
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
@@ -1246,7 +1300,23 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     else if (tag == ITEM_WSPHERE) rec = reinterpret_cast<const char*>(sc.spheres + GIX(idx, sc.n_spheres, 38));
     else if (is_inst) rec = reinterpret_cast<const char*>(sc.inst_entry + GIX(idx, sc.n_refs, 17));
     const rtg_f4u* const g = reinterpret_cast<const rtg_f4u*>(rec);
+#if RTG_GATHER_TRIM
+    // each lane loads only the rows its record uses (a one-triangle leaf 36 B,
+    // a leaf header 8 B, an instance exit nothing): the vector-memory path
+    // costs one L1 tag lookup per active lane and row
+    const bool tri_rec = item_is_tri_leaf(tag) || (kWide && item_is_wtri_leaf(tag));
+    const bool n0 = tag != ITEM_INST_END;
+    const bool n1 = n0 && tag != ITEM_LEAF;
+    const bool n2 = n1 && tag != ITEM_WSPHERE;
+    const bool n34 = n2 && !(tri_rec && (tag == ITEM_TRI1 || (kWide && tag == ITEM_WTRI1)));
+    rtg_f4u g0 = {0.0f, 0.0f, 0.0f, 0.0f}, g1 = g0, g2 = g0, g3 = g0, g4 = g0;
+    if (n0) g0 = g[0];
+    if (n1) g1 = g[1];
+    if (n2) g2 = g[2];
+    if (n34) { g3 = g[3]; g4 = g[4]; }
+#else
     const rtg_f4u g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4];
+#endif
     rtg_f4u g5 = {0.0f, 0.0f, 0.0f, 0.0f}, g6 = g5;
     if (is_inst) { g5 = g[5]; g6 = g[6]; }
     bool any = false;
@@ -1398,7 +1468,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
         }
       }
     } else {  // ITEM_INST_END: back to the world-space ray
-      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
+      T.cr = S.world_ray(); S.set_cur_ref(-1);
     }
 #ifdef RTG_STAMP
     const uint32_t sb = rtg_stamp();
@@ -1409,7 +1479,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     if (T.item == ITEM_POP || T.item == ITEM_NONE) T.item = pop();
     // leaving an instance: restore the world ray here, not in another round
     while (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) == ITEM_INST_END) {
-      T.cr.o = S.wo(); T.cr.d = S.wd(); T.cr.inv = S.winv(); S.set_cur_ref(-1);
+      T.cr = S.world_ray(); S.set_cur_ref(-1);
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE) postpone();

@@ -1261,6 +1261,51 @@ struct Flattener {
     S.sphere_wref.assign(S.spheres.size(), -1);
     for (size_t i = 0; i < n_tlas4; ++i)
       for (uint32_t& it : S.nodes4[i].item) it = inline_world_leaf(it);
+    hot_first_order();
+  }
+  // Node order for the traversal kernels' LDS node cache (trav_step
+  // kLdsNodes: nodes [0, K) are read from a per-block LDS copy): the world
+  // BVH's nodes breadth-first from its root, then the top levels of every
+  // BLAS breadth-first (all roots, then their children, ...), then every
+  // other node in its DFS order.  Node indices only name records, so the
+  // traversal, its counts and the hits are unchanged.
+  void hot_first_order() {
+    if (const char* e = std::getenv("RTGPU_HOT_FIRST"))   // A/B knob: 0 keeps the DFS order
+      if (std::atoi(e) == 0) return;
+    constexpr size_t kBlasTop = 256;   // BLAS nodes moved to the front (more than any K the kernels use)
+    const size_t n = S.nodes4.size();
+    std::vector<uint32_t> order;
+    order.reserve(n);
+    std::vector<char> taken(n, 0);
+    auto is_node = [](uint32_t it) { return (it >> ITEM_SHIFT) == ITEM_NODE; };
+    auto bfs = [&](std::vector<uint32_t> q, size_t limit) {
+      for (size_t h = 0; h < q.size() && order.size() < limit; ++h) {
+        const uint32_t i = q[h];
+        if (taken[i]) continue;
+        taken[i] = 1;
+        order.push_back(i);
+        for (uint32_t it : S.nodes4[i].item)
+          if (is_node(it)) q.push_back(it & ITEM_MASK);
+      }
+    };
+    if (is_node(S.tlas.root_item)) bfs({S.tlas.root_item & ITEM_MASK}, n);
+    std::vector<uint32_t> roots;
+    for (const DBvh& b : S.blas)
+      if (is_node(b.root_item)) roots.push_back(b.root_item & ITEM_MASK);
+    bfs(roots, order.size() + kBlasTop);
+    for (uint32_t i = 0; i < uint32_t(n); ++i)
+      if (!taken[i]) order.push_back(i);
+    std::vector<uint32_t> perm(n);
+    for (size_t k = 0; k < n; ++k) perm[order[k]] = uint32_t(k);
+    auto remap = [&](uint32_t& it) { if (is_node(it)) it = (ITEM_NODE << ITEM_SHIFT) | perm[it & ITEM_MASK]; };
+    std::vector<DNode4> out(n);
+    for (size_t k = 0; k < n; ++k) {
+      out[k] = S.nodes4[order[k]];
+      for (uint32_t& it : out[k].item) remap(it);
+    }
+    S.nodes4.swap(out);
+    remap(S.tlas.root_item);
+    for (DBvh& b : S.blas) remap(b.root_item);
   }
   // ---- BVH2 -> 8-wide nodes (DNode8, RT_NODES_WIDE8).  The same SAH-optimal
   // cut as collapse4 with up to eight child items per node (dp8_*: the least

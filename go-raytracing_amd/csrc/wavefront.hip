@@ -51,6 +51,28 @@
 #define RTG_SHADOW_WAVES RTG_TRAV_WAVES
 #endif
 #define RTG_SHADOW_WAVES_FOR(kVol, kCount) ((kCount) ? 4 : (kVol) ? RTG_VOL_WAVES : RTG_SHADOW_WAVES)
+// BVH4 nodes held in LDS per block (trav_step kLdsN; fp32 node format only),
+// in what the LDS leaves beside the stack ring at 7 waves per SIMD (160 KB
+// per CU, allocated in 512-B granules: at most 45 granules, 23040 B, per
+// block).  k_shadow: 16 words per lane (the world ray's 1/d recomputed on
+// instance exit) + 48 nodes = 22 KB.  k_extend keeps the 1/d in LDS
+// (RTG_EXT_WINV: 22 words per lane, room for 4 nodes, the top of the world
+// BVH): recomputing it there cost 4 % of its single-stream time, more than
+// 28 LDS nodes returned (DESIGN §3 "LDS node cache").
+#ifndef RTG_EXT_WINV
+#define RTG_EXT_WINV 1
+#endif
+#ifndef RTG_LDS_NODES_EXT
+#define RTG_LDS_NODES_EXT (RTG_EXT_WINV ? 4 : 28)
+#endif
+#ifndef RTG_LDS_NODES_SH
+#define RTG_LDS_NODES_SH 48
+#endif
+#ifndef RTG_LDS_NODES_TAIL
+#define RTG_LDS_NODES_TAIL 64
+#endif
+#define RTG_LDS_N(k, kQuant, kWide) (((kQuant) || (kWide)) ? 0 : (k))
+#define RTG_LDS_ARR(k) ((k) > 0 ? (k) * 8 : 1)
 
 namespace rtg {
 
@@ -269,6 +291,18 @@ __device__ __forceinline__ void wavetime_note(unsigned long long t0, uint32_t ra
 }
 #endif
 
+// Result stores (hit records, visibility words) through L2 (temporal), so a
+// wave's lanes finishing at different steps fill whole lines there before
+// they are written back, instead of one partial-line write each (VERDICT r4
+// #4: WRITE_SIZE 2.2x / 8x the record bytes with non-temporal stores)
+#ifndef RTG_RESULT_TEMPORAL
+#define RTG_RESULT_TEMPORAL 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st_result(V* p, V v) {
+  if (RTG_RESULT_TEMPORAL) *p = v;
+  else stnt(p, v);
+}
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
   const float4 r = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
@@ -277,7 +311,7 @@ __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_
   // diagnostic bound only (wrong frames): the store kept but never taken
   if (__float_as_uint(r.x) == 0x7FC00123u)
 #endif
-  stnt(&hit[p], r);
+  st_result(&hit[p], r);
 }
 
 // ---------------------------------------------------------------- extend
@@ -291,7 +325,11 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
                                                                 PathStream cs, const uint32_t* count,
                                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
                                                                 uint32_t* fetch, uint32_t sample_base) {
-  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack ring + world ray + hit record
+  constexpr bool kWinv = RTG_EXT_WINV != 0;
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + (kWinv ? kWorldInvWords : 0) + kHitWords) * 256];   // stack ring + world ray + hit record
+  constexpr int kLds = RTG_LDS_N(RTG_LDS_NODES_EXT, kQuant, kWide);
+  __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
+  lds_nodes_fill<kLds>(sc, lds_nodes);
   // next stream's count, the shadow job count and the shadow fetch counter
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *zero_a = 0u;
@@ -308,7 +346,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
   if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(60, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
 #endif
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
-                 a.spill_cap};
+                 a.spill_cap, lds_nodes, kWinv};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool P = pool_init();
@@ -354,7 +392,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<false, kCount, kVol, kQuant, kWide>(sc, T, S, cnt, a.err);
+      const int s = trav_step<false, kCount, kVol, kQuant, kWide, kLds>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
   }
@@ -815,13 +853,16 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
 template <int STACK, bool kVol, int kShade, bool kQuant, bool kWide>
 __global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                               const uint32_t* count, uint32_t* fetch) {
-  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kHitWords) * 256];   // stack ring + world ray + hit record
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kWorldInvWords + kHitWords) * 256];   // stack ring + world ray + hit record
+  constexpr int kLds = RTG_LDS_N(RTG_LDS_NODES_TAIL, kQuant, kWide);
+  __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
 #ifdef RTG_HOST_EMU
   static char s_dyn[kLdsMaterials * sizeof(DMaterial) + kLdsTextures * sizeof(DTexture) + kLdsLights * sizeof(DLight)];
 #else
   extern __shared__ char s_dyn[];   // shade_lds_bytes(sc), as k_shade
 #endif
   DScene sc = scg;
+  lds_nodes_fill<kLds>(sc, lds_nodes);
   if (kShade != SHADE_FULL || shade_tables_fit(sc)) {   // k_shade's LDS tables
     DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
     DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
@@ -840,7 +881,7 @@ __global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamer
   if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(66, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
 #endif
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
-                 a.spill_cap};
+                 a.spill_cap, lds_nodes, true};
   Cnt cnt = {};
   Trav T{};
   Pool Q = pool_init();
@@ -870,7 +911,7 @@ __global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamer
       if (Q.dry) break;
       continue;
     }
-    if (p != ITEM_NONE && !pending) pending = trav_step<false, false, kVol, kQuant, kWide>(sc, T, S, cnt, a.err) != TRAV_RUNNING;
+    if (p != ITEM_NONE && !pending) pending = trav_step<false, false, kVol, kQuant, kWide, kLds>(sc, T, S, cnt, a.err) != TRAV_RUNNING;
     while (p != ITEM_NONE && pending) {
       // the hit record k_extend would store (store_hit), then k_shade's shading
       Best b = trav_best(T, S);
@@ -911,6 +952,9 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   // runs (run_batches)
   constexpr bool kNeeAtomic = RTG_NEE_ATOMIC && !kEnvIS;
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
+  constexpr int kLds = RTG_LDS_N(RTG_LDS_NODES_SH, kQuant, kWide);
+  __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
+  lds_nodes_fill<kLds>(sc, lds_nodes);
   if (blockIdx.x == 0 && threadIdx.x == 0)   // next extend's segment counters
     for (uint32_t k = 0; k < kSegs; ++k) zero_c[k * kSegStride] = 0u;
   const uint32_t n = *count;
@@ -919,7 +963,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(61, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
 #endif
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
-                 a.spill_cap};
+                 a.spill_cap, lds_nodes};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool Q = pool_init();
@@ -954,7 +998,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
 #ifdef RTG_DIAG_NO_RESULT_STORES
     if (vis == 0xDEADu)
 #endif
-    if (!kNeeAtomic || a.keep_vis) stnt(&a.sj_vis[p], vis);
+    if (!kNeeAtomic || a.keep_vis) st_result(&a.sj_vis[p], vis);
     if (kNeeAtomic && (vis & 1u)) {
       // k_nee_apply's L + contribution, here: one float add per component in
       // the L2 atomic unit, with no return (the lane does not wait).  Within
@@ -1003,7 +1047,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       continue;
     }
     if (p != ITEM_NONE) {
-      const int s = trav_step<true, kCount, kVol, kQuant, kWide>(sc, T, S, cnt, a.err);
+      const int s = trav_step<true, kCount, kVol, kQuant, kWide, kLds>(sc, T, S, cnt, a.err);
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
   }
