@@ -3,6 +3,7 @@
 // exactly as rt_scene_upload does, and checks every index the kernels will
 // dereference.  Prints one JSON line; exit code 0 iff all checks pass.
 // Built and run by tests/test_flatten_host.py (g++, no GPU).
+#include <algorithm>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -123,6 +124,36 @@ int main(int argc, char** argv) {
                             seen_ref[L.first] > 0);
           CHECK(seen[it & ITEM_MASK] > 0 || inl, "BVH2 leaf not reached through the BVH4");
         }
+  }
+  // Hot-first node order (flatten.cpp hot_first_order, the kernels' LDS node
+  // cache holds nodes [0, K)): the world BVH breadth-first from index 0, then
+  // the BLAS roots, every child of a node in that front part numbered after it.
+  {
+    size_t n_world = 0;
+    if ((S.tlas.root_item >> ITEM_SHIFT) == ITEM_NODE) {
+      CHECK((S.tlas.root_item & ITEM_MASK) == 0u, "hot-first: world root not node 0");
+      std::vector<uint32_t> q{S.tlas.root_item & ITEM_MASK};
+      std::vector<char> in(S.nodes4.size(), 0);
+      for (size_t h = 0; h < q.size(); ++h) {
+        if (q[h] >= S.nodes4.size() || in[q[h]]) continue;
+        in[q[h]] = 1;
+        ++n_world;
+        for (uint32_t it : S.nodes4[q[h]].item)
+          if ((it >> ITEM_SHIFT) == ITEM_NODE) q.push_back(it & ITEM_MASK);
+      }
+      for (size_t i = 0; i < S.nodes4.size(); ++i) CHECK(bool(in[i]) == (i < n_world), "hot-first: world nodes not first");
+    }
+    size_t nroots = 0;
+    for (const DBvh& b : S.blas)
+      if ((b.root_item >> ITEM_SHIFT) == ITEM_NODE) {
+        CHECK((b.root_item & ITEM_MASK) >= n_world, "hot-first: BLAS root inside the world nodes");
+        ++nroots;
+      }
+    const size_t front = std::min(S.nodes4.size(), n_world + 64);
+    for (size_t i = 0; i < front; ++i)
+      for (uint32_t it : S.nodes4[i].item)
+        if ((it >> ITEM_SHIFT) == ITEM_NODE) CHECK((it & ITEM_MASK) > i, "hot-first: child numbered before its parent");
+    (void)nroots;
   }
   int culled = 0;
   for (size_t li = 0; li < S.leaves.size(); ++li) {
