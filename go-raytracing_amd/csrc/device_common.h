@@ -841,6 +841,10 @@ constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackV
 #define RTG_P2_SLACK 0
 #endif
 constexpr int kP2Slack = RTG_P2_SLACK;
+// Any-hit traversal without the near-to-far child sort (A/B knob)
+#ifndef RTG_ANY_NOSORT
+#define RTG_ANY_NOSORT 0
+#endif
 // The LDS node cache read through flat loads (one code path; A/B knob)
 #ifndef RTG_LDS_FLAT
 #define RTG_LDS_FLAT 0
@@ -1230,7 +1234,19 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
       const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
     };
-    if (!exact) { cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2); }
+    // (any-hit rays: RTG_ANY_NOSORT skips the sort, the first hit child in
+    // slot order is visited first; an unoccluded ray visits every child it
+    // enters whatever the order)
+    if (!exact && !(kAny && RTG_ANY_NOSORT)) { cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2); }
+    if (kAny && RTG_ANY_NOSORT) {
+      // the first hit child (slot order) into slot 0; the others are pushed
+      auto mv = [](float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
+        const bool sw = !(ta < __builtin_inff()) && tb < __builtin_inff();
+        const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
+        const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
+      };
+      mv(t0, i0, t1, i1); mv(t0, i0, t2, i2); mv(t0, i0, t3, i3);
+    }
 #ifdef RTG_STAMP
     const uint32_t st2 = rtg_stamp();
 #endif

@@ -284,7 +284,7 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
 // ray, so frames are unchanged.  RTG_CLAIM_PERM bits: 1 bounce-0 k_extend,
 // 2 k_shadow, 4 later k_extend bounces.
 #ifndef RTG_CLAIM_PERM
-#define RTG_CLAIM_PERM 0
+#define RTG_CLAIM_PERM 2
 #endif
 __device__ __forceinline__ uint32_t claim_perm(uint32_t idx, uint32_t n) {
   const uint32_t nb = n >> 6;

@@ -4,4 +4,4 @@
 # bounce (p7) against the default build; value, 2/4/8-way shard predictions.
 set -o pipefail
 mkdir -p gpurun_out
-REPS=${REPS:-2} tools/bal_ab.sh "lds::lib" "p1::lib_p1" "p3::lib_p3" "p7::lib_p7" 2>&1 | tee gpurun_out/r5_perm_bal.log
+REPS=${REPS:-2} bash tools/bal_ab.sh "lds::lib" "p1::lib_p1" "p3::lib_p3" "p7::lib_p7" 2>&1 | tee gpurun_out/r5_perm_bal.log
