@@ -841,6 +841,10 @@ constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackV
 #define RTG_P2_SLACK 0
 #endif
 constexpr int kP2Slack = RTG_P2_SLACK;
+// LDS node rows read at immediate offsets and picked by selects (A/B knob)
+#ifndef RTG_LDS_SEL
+#define RTG_LDS_SEL 0
+#endif
 // Any-hit traversal without the near-to-far child sort (A/B knob)
 #ifndef RTG_ANY_NOSORT
 #define RTG_ANY_NOSORT 0
@@ -1160,11 +1164,22 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       } else if (kLdsN > 0 && nidx < uint32_t(kLdsN)) {
         // the hot nodes from LDS: off the vector-memory path (TA / TD) that
         // the global node fetches saturate
+#if RTG_LDS_SEL
+        // all seven rows at immediate offsets from one address, near / far
+        // picked by selects (one address VGPR instead of six)
+        const float4* const lrow = S.ln + (nidx << 3);
+        const float4 xl = lrow[0], xh = lrow[1], yl = lrow[2], yh = lrow[3], zl = lrow[4], zh = lrow[5];
+        it = *reinterpret_cast<const uint4*>(lrow + 6);
+        nx = sxo ? xh : xl; fx = sxo ? xl : xh;
+        ny = syo ? yh : yl; fy = syo ? yl : yh;
+        nz = szo ? zh : zl; fz = szo ? zl : zh;
+#else
         const char* const lbase = reinterpret_cast<const char*>(S.ln);
         auto ldl = [&](uint32_t off) { return *reinterpret_cast<const float4*>(lbase + off); };
         nx = ldl(nb + sxo); fx = ldl(nb + (16u - sxo)); ny = ldl(nb + (32u + syo)); fy = ldl(nb + (48u - syo));
         nz = ldl(nb + (64u + szo)); fz = ldl(nb + (80u - szo));
         it = *reinterpret_cast<const uint4*>(lbase + (nb + 96u));
+#endif
       } else {
         const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
         auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };

@@ -507,7 +507,7 @@ __device__ __forceinline__ void shade_path(const DScene& sc, const DCamera& cam,
   }
 #endif
 #ifdef RTG_GUARD
-  if (kh == 0xFFFFFFFFu) rtg_guard_note(50, i, n);   // hit record never written by k_extend
+  if (kh == 0xFFFFFFFFu) rtg_guard_note(50, slot, bounce);   // hit record never written by k_extend
 #endif
   if (kh == 0u) {                                            // miss (camera.go:451-466)
     V3 bg;
