@@ -153,9 +153,28 @@ struct TRay {
   V3 o, d, inv;
 };
 typedef float f2 __attribute__((ext_vector_type(2)));
+// (A/B knob, off: bit-identical frames but the fallback branch spilled 10
+// more VGPRs in k_extend and 8 in k_shadow, C4 2146 -> 1970 Msamples/s)
+#ifndef RTG_RCP_EXACT
+#define RTG_RCP_EXACT 0
+#endif
+// 1/x rounded exactly as IEEE division rounds it: v_rcp_f32 (within 1 ulp)
+// and one FMA Newton step give the correctly rounded reciprocal for every x
+// whose exponent field lies in 2..252 (checked exhaustively over all 2^32
+// patterns on the GPU, tools/rcp/rcp_check.hip, profiles/r05_rcp_check.log);
+// zeros, denormals, |x| >= 2^126, infinities and NaNs take the division.
+__device__ __forceinline__ float rcp_exact(float x) {
+#if defined(RTG_HOST_EMU) || !RTG_RCP_EXACT
+  return 1.0f / x;
+#else
+  if (((__float_as_uint(x) >> 23) & 0xFFu) - 2u > 250u) return 1.0f / x;
+  const float r = __builtin_amdgcn_rcpf(x);
+  return fmaf(fmaf(-x, r, 1.0f), r, r);
+#endif
+}
 __device__ __forceinline__ TRay make_tray(V3 o, V3 d) {
   TRay r; r.o = o; r.d = d;
-  r.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // AABB.Hit adinv (aabb.go:64)
+  r.inv = mk(rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z));   // AABB.Hit adinv (aabb.go:64)
   return r;
 }
 
