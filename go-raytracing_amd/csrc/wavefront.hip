@@ -1087,6 +1087,9 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
 // contribution if visible), summed in that order (camera.go:549-558).
 // Without HDRI importance sampling a job carries beta * contribution already;
 // a job whose rays were all occluded adds zero and is skipped.
+#ifndef RTG_NEE_EAGER
+#define RTG_NEE_EAGER 0
+#endif
 template <bool kEnvIS>
 __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count) {
   const uint32_t n = *count;
@@ -1095,9 +1098,18 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
     const uint32_t kk = GIX(k, a.slots, 59);
     // (k_shadow sets a visibility bit only for a ray the job asked for, so
     // the job's flag word need not be read: vis & flags == vis)
+#if RTG_NEE_EAGER
+    // the job's contribution read with its visibility word (one dependent
+    // round trip less before the Lout read-modify-write; an occluded job's
+    // 16 B are read for nothing)
+    const uint32_t vis = ldnt(&a.sj_vis[kk]);
+    const float4 ea = ldnt(&a.ne_a[kk]);
+    if ((vis & 3u) == 0u) continue;
+#else
     const uint32_t vis = ldnt(&a.sj_vis[kk]);
     if ((vis & 3u) == 0u) continue;
     const float4 ea = ldnt(&a.ne_a[kk]);
+#endif
     float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
     const float4 L4 = ldnt(Lp);
     V3 L;
