@@ -65,6 +65,9 @@
 #ifndef RTG_LDS_NODES_EXT
 #define RTG_LDS_NODES_EXT (RTG_EXT_WINV ? 4 : 28)
 #endif
+#ifndef RTG_FIRST_NOINV
+#define RTG_FIRST_NOINV 0
+#endif
 #ifndef RTG_LDS_NODES_SH
 #define RTG_LDS_NODES_SH 48
 #endif
@@ -349,9 +352,11 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
                                                                 PathStream cs, const uint32_t* count,
                                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
                                                                 uint32_t* fetch, uint32_t sample_base) {
-  constexpr bool kWinv = RTG_EXT_WINV != 0;
+  // RTG_FIRST_NOINV: bounce 0's camera rays recompute the world 1/d and take
+  // 28 LDS nodes (A/B knob)
+  constexpr bool kWinv = RTG_EXT_WINV != 0 && !(kFirst && RTG_FIRST_NOINV);
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + (kWinv ? kWorldInvWords : 0) + kHitWords) * 256];   // stack ring + world ray + hit record
-  constexpr int kLds = RTG_LDS_N(RTG_LDS_NODES_EXT, kQuant, kWide);
+  constexpr int kLds = RTG_LDS_N(kWinv ? RTG_LDS_NODES_EXT : 28, kQuant, kWide);
   __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
   lds_nodes_fill<kLds>(sc, lds_nodes);
   // next stream's count, the shadow job count and the shadow fetch counter
