@@ -872,10 +872,6 @@ constexpr int kP2Slack = RTG_P2_SLACK;
 #ifndef RTG_LDS_FLAT
 #define RTG_LDS_FLAT 0
 #endif
-// Phase 2's record gather loads only the rows the lane's record uses (A/B knob)
-#ifndef RTG_GATHER_TRIM
-#define RTG_GATHER_TRIM 0
-#endif
 // BVH4 fp32 slab arithmetic in packed fp32 (v_pk_add_f32 / v_pk_mul_f32):
 // half the slab VALU instructions, bit-identical, but measured slower (C4
 // 2018 -> 1934 Msamples/s, k_extend 99.5 -> 107 ms per frame: 13 VGPRs
@@ -1350,23 +1346,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     else if (tag == ITEM_WSPHERE) rec = reinterpret_cast<const char*>(sc.spheres + GIX(idx, sc.n_spheres, 38));
     else if (is_inst) rec = reinterpret_cast<const char*>(sc.inst_entry + GIX(idx, sc.n_refs, 17));
     const rtg_f4u* const g = reinterpret_cast<const rtg_f4u*>(rec);
-#if RTG_GATHER_TRIM
-    // each lane loads only the rows its record uses (a one-triangle leaf 36 B,
-    // a leaf header 8 B, an instance exit nothing): the vector-memory path
-    // costs one L1 tag lookup per active lane and row
-    const bool tri_rec = item_is_tri_leaf(tag) || (kWide && item_is_wtri_leaf(tag));
-    const bool n0 = tag != ITEM_INST_END;
-    const bool n1 = n0 && tag != ITEM_LEAF;
-    const bool n2 = n1 && tag != ITEM_WSPHERE;
-    const bool n34 = n2 && !(tri_rec && (tag == ITEM_TRI1 || (kWide && tag == ITEM_WTRI1)));
-    rtg_f4u g0 = {0.0f, 0.0f, 0.0f, 0.0f}, g1 = g0, g2 = g0, g3 = g0, g4 = g0;
-    if (n0) g0 = g[0];
-    if (n1) g1 = g[1];
-    if (n2) g2 = g[2];
-    if (n34) { g3 = g[3]; g4 = g[4]; }
-#else
     const rtg_f4u g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4];
-#endif
     rtg_f4u g5 = {0.0f, 0.0f, 0.0f, 0.0f}, g6 = g5;
     if (is_inst) { g5 = g[5]; g6 = g[6]; }
     bool any = false;
