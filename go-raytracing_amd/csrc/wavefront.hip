@@ -181,6 +181,9 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 #endif
 // claim runs are 1/(RTG_GSS_DIV x waves per segment) of what a wave last
 // saw left in its segment
+#ifndef RTG_GSS_LAG
+#define RTG_GSS_LAG 0
+#endif
 #ifndef RTG_GSS_DIV
 #define RTG_GSS_DIV 4
 #endif
@@ -205,6 +208,11 @@ struct Pool {
   uint32_t tried;      // segments found drained
   bool dry;            // every segment is drained
   bool tail;           // the queue is nearly drained (runs at their minimum): stop prefetching
+  uint32_t lag;        // RTG_GSS_LAG: how far the counter moved while the wave traced its last run
+#ifdef RTG_WAVETIME
+  uint32_t nclaims = 0, lastrun = 0, steals = 0;   // diagnostic: the wave's claims, its last run, its steal claims
+  unsigned long long tlast = 0;                    // diagnostic: wall clock of the last claim
+#endif
 };
 __device__ __forceinline__ uint32_t xcc_id() {
 #ifdef RTG_HOST_EMU
@@ -217,9 +225,13 @@ __device__ __forceinline__ uint32_t xcc_id() {
 }
 __device__ __forceinline__ Pool pool_init() {
 #if RTG_XCD_SEGMENTS
-  return Pool{0u, 0u, xcc_id(), 0u, false, false};
+  Pool P{};
+  P.cur = 0u; P.end = 0u; P.seg = xcc_id(); P.tried = 0u; P.dry = false; P.tail = false; P.lag = 0u;
+  return P;
 #else
-  return Pool{0u, 0u, 0u, 0u, false, false};
+  Pool P{};
+  P.cur = 0u; P.end = 0u; P.seg = 0u; P.tried = 0u; P.dry = false; P.tail = false; P.lag = 0u;
+  return P;
 #endif
 }
 
@@ -251,14 +263,30 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
       // prefetched ray behind its current one: a ray left queued behind
       // another lane's long traversal would end the kernel that much later
       P.tail = RTG_NO_PREFETCH || (RTG_TAIL_NO_PREFETCH && run < 64u);
+#if RTG_GSS_LAG
+      // the run sized from the counter's extrapolated position: the wave's
+      // own last run end plus what the others claimed while it traced that
+      // run (a wave back from a long run would otherwise size its claim from
+      // a stale position and take a large run near the segment's end)
+      if (!P.tried) {
+        const uint32_t fx = hi - from > P.lag ? from + P.lag : hi;
+        run = (hi - fx) / (uint32_t(RTG_GSS_DIV) * wps);
+      }
+#endif
       run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
       uint32_t base = 0;
       if (__lane_id() == leader) base = atomicAdd(ctr + P.seg * kSegStride, run);
       // wave-uniform: scalar registers for the pool state
       base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + lo;
       if (base < hi) {
+#if RTG_GSS_LAG
+        P.lag = (!P.tried && P.end > lo && P.end <= hi && base > P.end) ? base - P.end : 0u;
+#endif
         P.cur = base;
         P.end = hi - base > run ? base + run : hi;
+#ifdef RTG_WAVETIME
+        P.nclaims++; P.lastrun = P.end - P.cur; P.tlast = wall_clock64(); P.steals += P.tried ? 1u : 0u;
+#endif
         break;
       }
       // this segment is drained: the next one (a wave every segment's
@@ -305,15 +333,20 @@ __device__ __forceinline__ uint32_t claim_perm(uint32_t idx, uint32_t n) {
 // and end on the 100 MHz wall clock and the rays it traced (run_batches
 // prints the distribution after each launch).  Vector stores from lane 0.
 constexpr int kWtWaves = 16384;
-__device__ unsigned long long rtg_wt[3 * kWtWaves];
-__device__ __forceinline__ void wavetime_note(unsigned long long t0, uint32_t rays) {
+constexpr int kWtWords = 6;
+__device__ unsigned long long rtg_wt[kWtWords * kWtWaves];
+__device__ __forceinline__ void wavetime_note(unsigned long long t0, uint32_t rays, const Pool& P) {
   const unsigned long long t1 = wall_clock64();
   for (int o = 32; o > 0; o >>= 1) rays += __shfl_xor(rays, o);
   const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (__lane_id() == 0 && w < uint32_t(kWtWaves)) {
-    rtg_wt[3 * w] = t0;
-    rtg_wt[3 * w + 1] = t1;
-    rtg_wt[3 * w + 2] = rays;
+    unsigned long long* r = rtg_wt + size_t(kWtWords) * w;
+    r[0] = t0;
+    r[1] = t1;
+    r[2] = rays;
+    r[3] = P.nclaims | (uint64_t(P.steals) << 32);
+    r[4] = P.tlast;
+    r[5] = P.lastrun;
   }
 }
 #endif
@@ -426,7 +459,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
     }
   }
 #ifdef RTG_WAVETIME
-  wavetime_note(wt0, wt_rays);
+  wavetime_note(wt0, wt_rays, P);
 #endif
 #ifdef RTG_STAMP
   add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
@@ -1220,17 +1253,43 @@ static hipError_t wavetime_report(const char* name, int bounce, int nwaves, hipS
   hipError_t e = hipStreamSynchronize(st);
   if (e != hipSuccess) return e;
   if (nwaves > kWtWaves) nwaves = kWtWaves;
-  std::vector<unsigned long long> h(size_t(3) * nwaves);
+  std::vector<unsigned long long> h(size_t(kWtWords) * nwaves);
   if ((e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rtg_wt), h.size() * sizeof(unsigned long long))) != hipSuccess) return e;
   unsigned long long t0 = ~0ull, s_last = 0;
-  for (int w = 0; w < nwaves; ++w) t0 = std::min(t0, h[3 * w]);
+  for (int w = 0; w < nwaves; ++w) t0 = std::min(t0, h[kWtWords * w]);
   std::vector<double> ends(nwaves), rays(nwaves);
   double tot = 0;
   for (int w = 0; w < nwaves; ++w) {
-    ends[w] = double(h[3 * w + 1] - t0) / 100.0;   // us
-    s_last = std::max(s_last, h[3 * w] - t0);
-    rays[w] = double(h[3 * w + 2]);
+    ends[w] = double(h[kWtWords * w + 1] - t0) / 100.0;   // us
+    s_last = std::max(s_last, h[kWtWords * w] - t0);
+    rays[w] = double(h[kWtWords * w + 2]);
     tot += rays[w];
+  }
+  {
+    // the last-ending 2 % of the waves against the rest: when they made their
+    // last claim, how big it was, how many claims and steals they made
+    std::vector<int> idx(nwaves);
+    for (int w = 0; w < nwaves; ++w) idx[w] = w;
+    std::sort(idx.begin(), idx.end(), [&](int x, int y) { return ends[x] < ends[y]; });
+    auto stats = [&](int from, int to, const char* tag) {
+      std::vector<double> lc, lr, nc, ns, gap;
+      for (int k = from; k < to; ++k) {
+        const int w = idx[k];
+        const unsigned long long* r = &h[size_t(kWtWords) * w];
+        lc.push_back(r[4] ? double(r[4] - t0) / 100.0 : 0.0);
+        lr.push_back(double(r[5]));
+        nc.push_back(double(r[3] & 0xFFFFFFFFull));
+        ns.push_back(double(r[3] >> 32));
+        gap.push_back(r[4] ? double(r[1] - r[4]) / 100.0 : 0.0);
+      }
+      auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
+      auto mx = [](const std::vector<double>& v) { return v.empty() ? 0.0 : *std::max_element(v.begin(), v.end()); };
+      fprintf(stderr, "RTG_WAVETIME   %s: last claim at med %.1f us, last run med %.0f max %.0f, claims med %.0f, steals med %.0f, last claim -> end med %.1f max %.1f us\n",
+              tag, med(lc), med(lr), mx(lr), med(nc), med(ns), med(gap), mx(gap));
+    };
+    const int cut = nwaves - std::max(1, nwaves / 50);
+    stats(0, cut, "first 98%");
+    stats(cut, nwaves, "last 2% ");
   }
   std::vector<double> se = ends, sr = rays;
   std::sort(se.begin(), se.end());
