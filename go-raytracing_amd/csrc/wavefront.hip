@@ -304,30 +304,6 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   return idx;
 }
 
-// Claim order -> queue position.  Claims hand out 64-position blocks in a
-// scattered order: block b of the last 2^k full blocks of the queue goes to
-// (b * mul) mod 2^k with an odd mul near 0.618 * 2^k, the first blocks and
-// the partial last block keep their place.  A wave's 64 lanes still take 64
-// neighbouring positions (4 rows of a 16x16 tile at bounce 0), but a claimed
-// run of several blocks spreads over the whole queue, so its cost is close
-// to the average instead of following one image region (the bounce-0 claim
-// tails).  The closest hit does not depend on which wave traces a
-// ray, so frames are unchanged.  RTG_CLAIM_PERM bits: 1 bounce-0 k_extend,
-// 2 k_shadow, 4 later k_extend bounces.
-#ifndef RTG_CLAIM_PERM
-#define RTG_CLAIM_PERM 2
-#endif
-__device__ __forceinline__ uint32_t claim_perm(uint32_t idx, uint32_t n) {
-  const uint32_t nb = n >> 6;
-  if (nb < 2u) return idx;
-  const uint32_t k = 31u - uint32_t(__builtin_clz(nb));   // 2^k <= nb
-  const uint32_t m = (1u << k) - 1u, first = nb - (1u << k);
-  const uint32_t b = idx >> 6;
-  if (b < first || b >= nb) return idx;
-  const uint32_t mul = (uint32_t((uint64_t(m + 1u) * 2654435769ull) >> 32)) | 1u;   // odd, ~0.618 * 2^k
-  return ((first + ((b - first) * mul & m)) << 6) | (idx & 63u);
-}
-
 #ifdef RTG_WAVETIME
 // Diagnostic builds only: per wave of the last traversal launch, its start
 // and end on the 100 MHz wall clock and the rays it traced (run_batches
