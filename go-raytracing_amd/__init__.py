@@ -38,6 +38,7 @@ RT_BLAS_REFERENCE, RT_BLAS_SAH, RT_BLAS_DEVICE = 0, 1, 2
 RT_NODES_FP32, RT_NODES_QUANT8, RT_NODES_WIDE8 = 0, 1, 2
 RT_OPT_DEALING, RT_OPT_DEAL_FIRST = 10, 11
 RT_OPT_TAIL = 12
+RT_OPT_OVERLAP = 13
 RT_DEAL_STATIC, RT_DEAL_DYNAMIC = 0, 1
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_SCENE", -6: "RT_ERR_DEVICE"}
@@ -553,6 +554,13 @@ class Context:
         long-tail kernel once at most n remain (deep scenes without lights).
         Never changes the image."""
         self.set_option(RT_OPT_TAIL, paths)
+
+    def set_overlap(self, mode: int = 0):
+        """RT_OPT_OVERLAP for the next renders: 0 automatic (on in scenes with
+        lights), 1 off, 2 on.  Bounce b's shadow rays and NEE adds run beside
+        bounce b + 1's closest-hit kernel on a second stream per part.  Never
+        changes the image."""
+        self.set_option(RT_OPT_OVERLAP, mode)
 
     def set_kernel_timing(self, enable: bool = True):
         self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))

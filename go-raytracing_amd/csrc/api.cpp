@@ -72,6 +72,12 @@ struct rt_ctx {
   int opt_tail = 0;                     // RT_OPT_TAIL: 0 automatic, 1 off, > 1 the rays-left threshold
   bool probing = false;                 // path_probe: every bounce through the wavefront kernels
   int opt_streams = 0;            // RT_OPT_STREAMS: 1..kMaxTwins twins (0 = automatic: kDefaultTwins)
+  int opt_overlap = 0;            // RT_OPT_OVERLAP: 0 automatic, 1 off, 2 on
+  // bounce overlap (WavePlan::overlap): each twin's k_shadow / k_nee_apply
+  // stream and the events that order it against the twin's own stream
+  // (created at the first overlapped render)
+  hipStream_t aux_st[kMaxTwins] = {};
+  hipEvent_t ev_shade[kMaxTwins] = {}, ev_nee[kMaxTwins] = {};
   // twins of the last render (render_wave): the second's stream, the join
   // events, and where each twin's hit records and pixels are
   hipStream_t twin_st[kMaxTwins - 1] = {};   // twins 1.. (twin 0 runs on the caller's stream)
@@ -91,7 +97,6 @@ struct rt_ctx {
   // between calls (pixels outside a call's buckets keep their values)
   DevBuf frame, frame_rgba, frame_buckets;
   size_t frame_n = 0;
-  hipEvent_t twin_off_ev = nullptr;   // twin phase offset (WavePlan::offset_ev)
   hipEvent_t fan_ev = nullptr;    // caller-stream point the devices' renders start after
   hipEvent_t join_ev = nullptr;   // end of this device's share of a render
   // RT_OPT_DEALING: how a multi-device render deals its tiles (set on the
@@ -303,6 +308,9 @@ int check_render_error(rt_ctx* ctx, bool wait) {
 // shards (101 M) alike (3.73 / 3.74 vs 3.75 / 3.75; round 4).
 constexpr int kDefaultTwins = 2;
 constexpr uint64_t kThreeTwinSamples = uint64_t(1) << 26;
+// With the bounce overlap each twin runs two streams: at most two twins, so
+// that the four streams keep a hardware queue each (GPU_MAX_HW_QUEUES = 4).
+constexpr int kOverlapTwins = 2;
 
 // Wavefront render (wavefront.hip): pixel list from the tiles, path-slot
 // batches sized to keep ~4M paths in flight.
@@ -324,7 +332,16 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // three parts 1605 / 1563 / 1557 Msamples/s (round 4).
   const int auto_twins = ctx->dscene.shade_kind == SHADE_VOL ? 1
                          : tile_px * uint64_t(std::max(1, p->samples_per_pixel)) > kThreeTwinSamples ? 3 : kDefaultTwins;
-  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : auto_twins;
+  // Bounce overlap (run_batches) for scenes with lights: a second stream per
+  // twin.  RTGPU_OVERLAP (tuning knob) / RT_OPT_OVERLAP: 1 off, 2 on.
+  static const int env_overlap = [] {
+    const char* e = getenv("RTGPU_OVERLAP");
+    return e ? atoi(e) : 0;
+  }();
+  const int ovl_opt = ctx->opt_overlap ? ctx->opt_overlap : env_overlap;
+  const bool overlap = ctx->dscene.num_lights > 0 && ovl_opt != 1;
+  const int auto_twins2 = overlap ? std::min(auto_twins, kOverlapTwins) : auto_twins;
+  const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : auto_twins2;
   const int nt = int(std::max<size_t>(1, std::min<size_t>(size_t(want_twins), tiles.size())));
   std::vector<uint32_t>& px = ctx->pix_host;
   px.clear();
@@ -368,13 +385,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // CNT_WORDS_Q queue counters plus two job words per slot: room for
   // kMaxTwins twins' counters whatever `nt` this render uses (S_t sum to
   // nslots over the twins).
-  size_t wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
-#ifdef RTG_GUARD
-  // RTGPU_GUARD_OLD_WQ=1 (diagnostic builds only): the round-3 sizing (two
-  // twins' counters), to show what its overflow does
-  static const bool old_wq = getenv("RTGPU_GUARD_OLD_WQ") && atoi(getenv("RTGPU_GUARD_OLD_WQ")) > 0;
-  if (old_wq) wq_bytes = (nslots * 2 + 2 * size_t(CNT_WORDS_Q)) * sizeof(uint32_t);
-#endif
+  const size_t wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
   if (ctx->wslots < nslots) {
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
@@ -398,32 +409,34 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   std::memcpy(ctx->pix_pinned, px.data(), npix * sizeof(uint32_t));
   HIPCHK(hipMemcpyAsync(ctx->wpix.p, ctx->pix_pinned, npix * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(ctx->pix_ev, st));
-#ifdef RTG_STAMP
-  HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
-#else
   if (count) HIPCHK(hipMemsetAsync(ctx->counters.p, 0, CNT_WORDS * sizeof(unsigned long long), st));
-#endif
   // lanes that must want an item before a wave claims a new run (pool_take):
   // within [1, 64] (the wave size), or no wave would ever claim
   static const int refill = [] {
     const char* e = getenv("RTGPU_REFILL");
     return e ? std::min(64, std::max(1, atoi(e))) : 16;
   }();
-  // LDS stack ring (8 entries per lane by default, 16 with RTGPU_STACK=16) +
-  // global spill up to kStackMax: scenes of any supported depth run with the
-  // small ring.
-  static const int lds_stack = [] {
-    const char* e = getenv("RTGPU_STACK");
-#ifdef RTG_RING24
-    if (e && atoi(e) == 24) return 24;   // diagnostic build only
+  // LDS stack ring (kLdsStack entries per lane) + global spill up to
+  // kStackMax: scenes of any supported depth run with the small ring.
+#ifdef RTG_DIAG_RING
+  const int stack = RTG_DIAG_RING;   // diagnostic builds (RTG_GUARD): the ring they were compiled for
+#else
+  const int stack = kLdsStack;
 #endif
-    return e && atoi(e) == 16 ? 16 : 8;
-  }();
-  const int stack = lds_stack;
   const uint32_t spill_lanes = uint32_t(std::max(1, ctx->num_cus)) * kSpillLanesPerCU;
-  const int spill_cap = kStackMax - stack;
-  const size_t spill_words = size_t(spill_lanes) * size_t(spill_cap);   // one twin's spill area
-  if ((rc = ensure(ctx, ctx->wspill, size_t(nt) * spill_words * sizeof(uint32_t)))) return rc;
+  // spill entries per lane: what the scene's stack bound leaves beyond the
+  // ring (flatten: stack_needed <= kStackMax; a deeper push is flagged)
+  const int spill_cap = std::max(1, std::min(kStackMax, int(ctx->dscene.stack_needed)) - stack);
+  const size_t spill_words = size_t(spill_lanes) * size_t(spill_cap);   // one spill area
+  // one area per twin, two with the bounce overlap (k_shadow beside k_extend)
+  const int spill_areas = nt * (overlap ? 2 : 1);
+  if ((rc = ensure(ctx, ctx->wspill, size_t(spill_areas) * spill_words * sizeof(uint32_t)))) return rc;
+  if (overlap && !ctx->aux_st[0])
+    for (int t = 0; t < kMaxTwins; ++t) {
+      HIPCHK(hipStreamCreateWithFlags(&ctx->aux_st[t], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ctx->ev_shade[t], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&ctx->ev_nee[t], hipEventDisableTiming));
+    }
   // each twin: kSlotF4 arrays of its own S_t slots, its queue counters and
   // job words, its slice of the pixel list and the fp64 sums, its spill area
   WaveArgs as[kMaxTwins]{};
@@ -459,18 +472,15 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     a.spill_lanes = spill_lanes;
     a.spill_cap = spill_cap;
     a.spill = static_cast<uint32_t*>(ctx->wspill.p) + size_t(t) * spill_words;
+    a.spill_sh = overlap ? static_cast<uint32_t*>(ctx->wspill.p) + size_t(nt + t) * spill_words : a.spill;
     a.slots = uint32_t(S);
     a.out_pixels = uint32_t(dc.width) * uint32_t(dc.height);
-    a.keep_vis = ctx->probing ? 1 : 0;
     ctx->twin_args[t] = a;
   }
   // the twins' slices must lie inside the batch buffers (an internal error
   // otherwise: nothing is launched)
   const size_t f4_used = size_t(fbase - static_cast<float4*>(ctx->wstate.p)) * sizeof(float4);
   const size_t q_used = size_t(qbase - static_cast<uint32_t*>(ctx->wq.p)) * sizeof(uint32_t);
-#ifdef RTG_GUARD
-  if (!old_wq)
-#endif
   if (f4_used > ctx->wstate.bytes || q_used > ctx->wq.bytes || q_used > wq_bytes)
     return set_err(ctx, RT_ERR_INVALID, "internal: twin buffers exceed the batch allocation");
   ctx->num_twins = nt;
@@ -487,11 +497,10 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   }();
   plan.max_blocks = ctx->opt_blocks ? ctx->opt_blocks : env_blocks;
   plan.num_twins = nt;
-  static const int env_offset = [] {
-    const char* e = getenv("RTGPU_TWIN_OFFSET");
-    return e ? atoi(e) : 0;
-  }();
-  plan.offset_ev = env_offset ? ctx->twin_off_ev : nullptr;
+  plan.overlap = overlap ? 1 : 0;
+  plan.aux = ctx->aux_st;
+  plan.ev_shade = ctx->ev_shade;
+  plan.ev_nee = ctx->ev_nee;
   static const int debug_sync = [] {
     const char* e = getenv("RTGPU_DEBUG_SYNC");
     return e && atoi(e) > 0 ? 1 : 0;
@@ -535,7 +544,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
     HIPCHK(hipEventRecord(ctx->twin_ev0, st));
     for (int t = 1; t < nt; ++t) HIPCHK(hipStreamWaitEvent(ctx->twin_st[t - 1], ctx->twin_ev0, 0));
   }
-  HIPCHK(launch_wavefront(ctx->dscene, dc, as, sts, plan, stack, count, d_out, p->accumulate ? 1 : 0));
+  HIPCHK(launch_wavefront(ctx->dscene, dc, as, sts, plan, count, d_out, p->accumulate ? 1 : 0));
   for (int t = 1; t < nt; ++t) {   // ... and the caller's stream continues once they have finished
     HIPCHK(hipEventRecord(ctx->twin_end[t - 1], ctx->twin_st[t - 1]));
     HIPCHK(hipStreamWaitEvent(st, ctx->twin_end[t - 1], 0));
@@ -548,23 +557,6 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   HIPCHK(hipMemcpyAsync(ctx->err_pinned, ctx->errflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(ctx->err_ev, st));
   ctx->err_pending = true;
-#ifdef RTG_STAMP
-  if (!count) {   // diagnostic build: per-kernel segment cycles of the traversal (wave sums)
-    unsigned long long c[CNT_WORDS];
-    HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipMemcpy(c, ctx->counters.p, sizeof c, hipMemcpyDeviceToHost));
-    for (int k : {int(KC_EXTEND), int(KC_SHADOW)}) {
-      const unsigned long long* b = c + k * CNT_BLOCK;
-      const double steps = double(b[20] ? b[20] : 1);
-      fprintf(stderr, "RTG_STAMP %s node-steps %llu cycles/step: load %.1f math %.1f rest %.1f | phase2 total %.3g (%.1f/step)\n",
-              k == KC_EXTEND ? "extend" : "shadow", b[20], b[16] / steps, b[17] / steps, b[18] / steps, double(b[19]),
-              b[19] / steps);
-      const double rounds = double(b[14] ? b[14] : 1);
-      fprintf(stderr, "RTG_STAMP %s phase-2 rounds %llu cycles/round: leaf %.1f inst %.1f inst_end %.1f tail %.1f\n",
-              k == KC_EXTEND ? "extend" : "shadow", b[14], b[21] / rounds, b[22] / rounds, b[23] / rounds, b[15] / rounds);
-    }
-  }
-#endif
 #ifdef RTG_GUARD
   {   // diagnostic build: report the first out-of-range index of this render
     unsigned int gr[4] = {0, 0, 0, 0};
@@ -755,7 +747,6 @@ int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 static bool create_twin_streams(rt_ctx* ctx) {
   if (hipEventCreateWithFlags(&ctx->twin_ev0, hipEventDisableTiming) != hipSuccess) return false;
-  if (hipEventCreateWithFlags(&ctx->twin_off_ev, hipEventDisableTiming) != hipSuccess) return false;
   for (int t = 0; t + 1 < kMaxTwins; ++t)
     if (hipStreamCreateWithFlags(&ctx->twin_st[t], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->twin_end[t], hipEventDisableTiming) != hipSuccess)
@@ -867,7 +858,11 @@ void rt_ctx_destroy(rt_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev1);
   if (ctx->fan_ev) (void)hipEventDestroy(ctx->fan_ev);
   if (ctx->twin_ev0) (void)hipEventDestroy(ctx->twin_ev0);
-  if (ctx->twin_off_ev) (void)hipEventDestroy(ctx->twin_off_ev);
+  for (int t = 0; t < kMaxTwins; ++t) {
+    if (ctx->aux_st[t]) { (void)hipStreamSynchronize(ctx->aux_st[t]); (void)hipStreamDestroy(ctx->aux_st[t]); }
+    if (ctx->ev_shade[t]) (void)hipEventDestroy(ctx->ev_shade[t]);
+    if (ctx->ev_nee[t]) (void)hipEventDestroy(ctx->ev_nee[t]);
+  }
   for (int t = 0; t + 1 < kMaxTwins; ++t) {
     if (ctx->twin_end[t]) (void)hipEventDestroy(ctx->twin_end[t]);
     if (ctx->twin_st[t]) { (void)hipStreamSynchronize(ctx->twin_st[t]); (void)hipStreamDestroy(ctx->twin_st[t]); }
@@ -926,6 +921,11 @@ int rt_ctx_set_option(rt_ctx* ctx, int32_t key, int32_t value) {
   if (key == RT_OPT_STREAMS) {
     if (value < 0 || value > kMaxTwins) return set_err(ctx, RT_ERR_INVALID, "streams must be 0 (default) or 1..4");
     ctx->opt_streams = value;
+    return RT_OK;
+  }
+  if (key == RT_OPT_OVERLAP) {
+    if (value < 0 || value > 2) return set_err(ctx, RT_ERR_INVALID, "overlap must be 0 (default), 1 (off) or 2 (on)");
+    ctx->opt_overlap = value;
     return RT_OK;
   }
   if (key == RT_OPT_TAIL) {
@@ -1504,7 +1504,7 @@ int path_probe(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sa
         HIPCHK(launch_path_hits(ctx->dscene, dc, a.hit, a.s[c].o, a.s[c].d, a.counts + (c ? CNT_STREAM1 : CNT_STREAM0),
                                 a.pixels, a.npix, seed, uint32_t(sample), bounce, top, prim, t, ray, ctx->stream));
       if (what & 2)
-        HIPCHK(launch_nee_probe(a.sj_info, a.sj_vis, a.ne_a, a.counts + CNT_SHADOW, a.pixels, a.npix, nee, ctx->stream));
+        HIPCHK(launch_nee_probe(a.sj_info, a.sj_vis, a.ne_a, a.counts + cnt_shadow(c), a.pixels, a.npix, nee, ctx->stream));
     }
   }
   if (out_top) HIPCHK(hipMemcpyAsync(out_top, top, n * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -153,28 +153,9 @@ struct TRay {
   V3 o, d, inv;
 };
 typedef float f2 __attribute__((ext_vector_type(2)));
-// (A/B knob, off: bit-identical frames but the fallback branch spilled 10
-// more VGPRs in k_extend and 8 in k_shadow, C4 2146 -> 1970 Msamples/s)
-#ifndef RTG_RCP_EXACT
-#define RTG_RCP_EXACT 0
-#endif
-// 1/x rounded exactly as IEEE division rounds it: v_rcp_f32 (within 1 ulp)
-// and one FMA Newton step give the correctly rounded reciprocal for every x
-// whose exponent field lies in 2..252 (checked exhaustively over all 2^32
-// patterns on the GPU, tools/rcp/rcp_check.hip, profiles/r05_rcp_check.log);
-// zeros, denormals, |x| >= 2^126, infinities and NaNs take the division.
-__device__ __forceinline__ float rcp_exact(float x) {
-#if defined(RTG_HOST_EMU) || !RTG_RCP_EXACT
-  return 1.0f / x;
-#else
-  if (((__float_as_uint(x) >> 23) & 0xFFu) - 2u > 250u) return 1.0f / x;
-  const float r = __builtin_amdgcn_rcpf(x);
-  return fmaf(fmaf(-x, r, 1.0f), r, r);
-#endif
-}
 __device__ __forceinline__ TRay make_tray(V3 o, V3 d) {
   TRay r; r.o = o; r.d = d;
-  r.inv = mk(rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z));   // AABB.Hit adinv (aabb.go:64)
+  r.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // AABB.Hit adinv (aabb.go:64)
   return r;
 }
 
@@ -411,32 +392,11 @@ __device__ __forceinline__ bool tie_wins(const DScene& sc, int kind, int refpos,
 // Work counters for the instrumented variant (rt_count_work).
 struct Cnt {
   uint32_t rays, shadow, nodes, sph, quad, tri, plane, inst, vol, mat, env, ibox, spill;
-#ifdef RTG_STAMP
-  // diagnostic build: s_memtime cycle sums of the traversal's segments, taken
-  // by the first active lane of the wave (so the lane sums are wave sums)
-  uint32_t st_load, st_math, st_rest, st_p2, st_steps, st_leaf, st_inst, st_end, st_tail, st_rounds;
-#endif
 };
-#ifdef RTG_STAMP
-__device__ __forceinline__ uint32_t rtg_stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return uint32_t(t);
-}
-__device__ __forceinline__ bool rtg_lead() { return __lane_id() == uint32_t(__ffsll(__ballot(1)) - 1); }
-#endif
-
 // Volume.Hit (volume.go:34-79) against a boundary given as an instance chain
 // over a list leaf.  ntests = how many times the enclosing leaf calls Hit
 // (2 for the BVHNode{leaf,leaf} wrapper): the reference then keeps the
 // smaller of the independent free-flight draws, i.e. U = max(U_1..U_n).
-#if defined(RTG_VOLUME_NOINLINE) && !defined(RTG_HOST_EMU)
-#define RTG_VOLUME_ATTR __attribute__((noinline))
-#else
-#define RTG_VOLUME_ATTR
-#endif
 // The end of Volume.Hit (volume.go:56-79) once the boundary's two closest
 // distances are known: clamp to the ray interval, the free flight
 // -(1/rho) ln U from the largest of the leaf's `ntests` draws, the hit.
@@ -462,7 +422,7 @@ __device__ __forceinline__ bool volume_flight(const DVolume& vol, V3 wd, bool h1
 }
 
 template <bool kCount>
-__device__ RTG_VOLUME_ATTR bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, float time,
+__device__ bool volume_hit(const DScene& sc, const DVolume& vol, V3 wo, V3 wd, float time,
                            float tmin, float tmax, int ntests, uint32_t key, uint32_t bounce,
                            uint32_t dom, float& t_out, Cnt& cnt) {
   const DInstance& bi = sc.instances[GIX(vol.boundary, sc.n_instances, 1)];
@@ -769,12 +729,7 @@ struct TStack {
   __device__ __forceinline__ int hit_idx() const { return hitp()[0] & 0x0FFFFFFF; }
   __device__ __forceinline__ int hit_refpos() const { return hitp()[stride]; }
   __device__ __forceinline__ int hit_primpos() const { return hitp()[2 * stride]; }
-#ifdef RTG_RING24
-  // diagnostic build only: a 24-entry ring is not a power of two
-  __device__ __forceinline__ int ring(int sp) const { return int(uint32_t(sp) % uint32_t(cap)); }
-#else
   __device__ __forceinline__ int ring(int sp) const { return sp & (cap - 1); }
-#endif
   // The depth bound (cap + spill_cap) is checked only on the spill path: the
   // common push / pop is one LDS access and one compare against the
   // compile-time ring size.  Past the bound (an internal error: the host
@@ -845,11 +800,9 @@ __device__ __forceinline__ void resolve_inst(const DScene& sc, Best& b) {
 // run of several blocks spreads over the whole queue, so its cost is close
 // to the average instead of following one image region (the bounce-0 claim
 // tails).  The closest hit does not depend on which wave traces a
-// ray, so frames are unchanged.  RTG_CLAIM_PERM bits: 1 bounce-0 k_extend,
-// 2 k_shadow, 4 later k_extend bounces.
-#ifndef RTG_CLAIM_PERM
-#define RTG_CLAIM_PERM 2
-#endif
+// ray, so frames are unchanged.  Used by k_shadow's job claims (C4 2134 /
+// 2137 -> 2159 / 2161 Msamples/s); on k_extend's claims it measured slower
+// (bounce 0: the same; every bounce: origin coherence lost).
 __device__ __forceinline__ uint32_t claim_perm(uint32_t idx, uint32_t n) {
   const uint32_t nb = n >> 6;
   if (nb < 2u) return idx;
@@ -866,48 +819,14 @@ enum : int { TRAV_RUNNING = 0, TRAV_DONE = 1, TRAV_ANYHIT = 2 };
 // Phase 1 of a while-while round ends once at most this many lanes of the
 // wave still lack a postponed leaf / instance item (0 = every lane holds one,
 // Aila & Laine's rule).  The last few lanes' node walks otherwise hold the
-// whole wave in phase 1 while the others wait.
-#ifndef RTG_P1_SLACK
-#define RTG_P1_SLACK 16
-#endif
-#ifndef RTG_P1_SLACK_ANY
-#define RTG_P1_SLACK_ANY RTG_P1_SLACK
-#endif
-// The rare-primitive (fog) variants measured best at 0: CornellBoxScene 985
-// vs 956 Msamples/s at 16; CornellBoxLucy 1445 at 0, 1662 at 4, 1770 at 16,
-// 1756 at 24, 1720 at 32, 1507 at 48.
-#ifndef RTG_P1_SLACK_VOL
-#define RTG_P1_SLACK_VOL 0
-#endif
-constexpr int kP1Slack = RTG_P1_SLACK, kP1SlackAny = RTG_P1_SLACK_ANY, kP1SlackVol = RTG_P1_SLACK_VOL;
-#ifndef RTG_P2_SLACK
-#define RTG_P2_SLACK 0
-#endif
-constexpr int kP2Slack = RTG_P2_SLACK;
-// LDS node rows read at immediate offsets and picked by selects (A/B knob)
-#ifndef RTG_LDS_SEL
-#define RTG_LDS_SEL 0
-#endif
-// Any-hit traversal without the near-to-far child sort (A/B knob)
-#ifndef RTG_ANY_NOSORT
-#define RTG_ANY_NOSORT 0
-#endif
-// The LDS node cache read through flat loads (one code path; A/B knob)
-#ifndef RTG_LDS_FLAT
-#define RTG_LDS_FLAT 0
-#endif
-// BVH4 fp32 slab arithmetic in packed fp32 (v_pk_add_f32 / v_pk_mul_f32):
-// half the slab VALU instructions, bit-identical, but measured slower (C4
-// 2018 -> 1934 Msamples/s, k_extend 99.5 -> 107 ms per frame: 13 VGPRs
-// spilled at the 72-register cap and the packed ops issue no faster than
-// two scalar ones, MI355X_MICROARCH.md); kept as a diagnostic variant
-#ifndef RTG_PK_SLAB
-#define RTG_PK_SLAB 0
-#endif
+// whole wave in phase 1 while the others wait.  CornellBoxLucy 1445 at 0,
+// 1662 at 4, 1770 at 16, 1756 at 24, 1720 at 32, 1507 at 48.  The
+// rare-primitive (fog) variants keep 0: CornellBoxScene 985 vs 956 at 16.
+constexpr int kP1Slack = 16, kP1SlackVol = 0;
 
 // Schedule independence of the closest hit (DESIGN §3 "Determinism").  The
 // result must not depend on which rays share a wave or on when a wave runs:
-//   * closest-hit phase 1 is not speculative (RTG_P1_SPECULATE 0): a lane
+//   * closest-hit phase 1 is not speculative: a lane
 //     that reaches a leaf / instance item stops walking nodes until it has
 //     processed it, so
 //     every lane performs the sequential near-first traversal's operations in
@@ -915,16 +834,9 @@ constexpr int kP2Slack = RTG_P2_SLACK;
 //     walk tests nodes against a closest distance that depends on how long
 //     the wave stays in phase 1);
 //   * a box is culled against the closest distance widened by 8 ulps
-//     (RTG_CULL_WIDEN, cull_widen): a primitive at t <= t_best whose box
+//     (cull_widen): a primitive at t <= t_best whose box
 //     entry rounds a few ulps above t_best is still reached, so the box test
 //     never decides the winner.
-#ifndef RTG_P1_SPECULATE
-#define RTG_P1_SPECULATE 0
-#endif
-#ifndef RTG_CULL_WIDEN
-#define RTG_CULL_WIDEN 1
-#endif
-constexpr bool kP1Speculate = RTG_P1_SPECULATE != 0;
 // The widened bound is what the closest-hit register T.bt holds, so the node
 // loop culls against it with no extra instruction (a multiply there cost 7
 // VGPR spills at the 72-register cap, 4 % of the frame): 8 ulps above the
@@ -932,7 +844,7 @@ constexpr bool kP1Speculate = RTG_P1_SPECULATE != 0;
 // Positive finite distances only (t >= tmin > 0); +inf stays +inf (a bit
 // pattern past +inf would be a NaN, which fmaxf / fminf would not ignore
 // the same way on every path).
-constexpr uint32_t kCullUlps = RTG_CULL_WIDEN ? 8u : 0u;
+constexpr uint32_t kCullUlps = 8u;
 __device__ __forceinline__ float cull_widen(float t) {
   const uint32_t b = __float_as_uint(t);
   const uint32_t w = b + kCullUlps;
@@ -1049,20 +961,16 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     S.push(T.sp, v, err);
     ++T.sp;
   };
-  // postpone the current leaf / instance item; the speculative variant pops
-  // the next stack entry and keeps walking nodes (leaves only: entering an
-  // instance changes the stack).  Any-hit rays always speculate: their result
-  // (is there a hit in [tmin, tmax]) does not depend on the visiting order.
+  // postpone the current leaf / instance item.  Any-hit rays pop the next
+  // stack entry and keep walking nodes (speculatively; leaves only: entering
+  // an instance changes the stack): their result (is there a hit in [tmin,
+  // tmax]) does not depend on the visiting order.
   auto postpone = [&]() {
     T.lf = T.item;
-    T.item = ((kP1Speculate || kAny) && item_is_leaf(T.lf)) ? pop() : ITEM_POP;
+    T.item = (kAny && item_is_leaf(T.lf)) ? pop() : ITEM_POP;
   };
   // ---------------- phase 1: internal nodes (BVH4)
   while (T.item < ITEM_POP && (T.item >> ITEM_SHIFT) == ITEM_NODE) {
-#ifdef RTG_STAMP
-    const bool st_lead = rtg_lead();
-    const uint32_t st0 = rtg_stamp();
-#endif
     const float hi = kAny ? T.tmax : exact ? best_t(T) : T.bt;
     const float inf = __builtin_inff();
     if constexpr (kWide) {
@@ -1089,9 +997,6 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       asm volatile("" ::"v"(h0.x), "v"(h0.y), "v"(h0.z), "v"(h0.w), "v"(h1.x), "v"(h1.y), "v"(h1.z), "v"(h1.w));
       asm volatile("" ::"v"(rx.x), "v"(rx.y), "v"(rx.z), "v"(rx.w), "v"(ry.x), "v"(ry.y), "v"(ry.z), "v"(ry.w));
       asm volatile("" ::"v"(rz.x), "v"(rz.y), "v"(rz.z), "v"(rz.w));
-#endif
-#ifdef RTG_STAMP
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
       const float stx = __uint_as_float(h1.y & 0xFFFF0000u), sty = __uint_as_float(h1.y << 16),
                   stz = __uint_as_float(h1.z & 0xFFFF0000u);
@@ -1160,14 +1065,11 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const float4 f1 = *reinterpret_cast<const float4*>(nbase + (nb + 16u));    // step yz, xlo xhi rows
       const uint4 ryz = *reinterpret_cast<const uint4*>(nbase + (nb + 32u));     // ylo yhi zlo zhi rows
       it = *reinterpret_cast<const uint4*>(nbase + (nb + 48u));
-#if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
+#if !defined(RTG_HOST_EMU)
       // issue the child-item load with the plane loads (same line): the
       // compiler otherwise sinks it into the "a child was hit" branch, which
       // costs a second dependent round trip per node
       asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));
-#endif
-#ifdef RTG_STAMP
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
       const float ax = (f0.x - T.cr.o.x) * T.cr.inv.x, bx = T.cr.inv.x * f0.w;
       const float ay = (f0.y - T.cr.o.y) * T.cr.inv.y, by = T.cr.inv.y * f1.x;
@@ -1192,70 +1094,24 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const uint32_t sxo = (__float_as_uint(T.cr.inv.x) >> 27) & 16u, syo = (__float_as_uint(T.cr.inv.y) >> 27) & 16u,
                      szo = (__float_as_uint(T.cr.inv.z) >> 27) & 16u;
       float4 nx, fx, ny, fy, nz, fz;
-      if (RTG_LDS_FLAT && kLdsN > 0) {
-        // one flat-load path: the lane's node base in LDS or in global memory
-        const char* const fbase = nidx < uint32_t(kLdsN) ? reinterpret_cast<const char*>(S.ln)
-                                                         : reinterpret_cast<const char*>(sc.nodes);
-        auto ldf = [&](uint32_t off) { return *reinterpret_cast<const float4*>(fbase + off); };
-        nx = ldf(nb + sxo); fx = ldf(nb + (16u - sxo)); ny = ldf(nb + (32u + syo)); fy = ldf(nb + (48u - syo));
-        nz = ldf(nb + (64u + szo)); fz = ldf(nb + (80u - szo));
-        it = *reinterpret_cast<const uint4*>(fbase + (nb + 96u));
-      } else if (kLdsN > 0 && nidx < uint32_t(kLdsN)) {
+      if (kLdsN > 0 && nidx < uint32_t(kLdsN)) {
         // the hot nodes from LDS: off the vector-memory path (TA / TD) that
         // the global node fetches saturate
-#if RTG_LDS_SEL
-        // all seven rows at immediate offsets from one address, near / far
-        // picked by selects (one address VGPR instead of six)
-        const float4* const lrow = S.ln + (nidx << 3);
-        const float4 xl = lrow[0], xh = lrow[1], yl = lrow[2], yh = lrow[3], zl = lrow[4], zh = lrow[5];
-        it = *reinterpret_cast<const uint4*>(lrow + 6);
-        nx = sxo ? xh : xl; fx = sxo ? xl : xh;
-        ny = syo ? yh : yl; fy = syo ? yl : yh;
-        nz = szo ? zh : zl; fz = szo ? zl : zh;
-#else
         const char* const lbase = reinterpret_cast<const char*>(S.ln);
         auto ldl = [&](uint32_t off) { return *reinterpret_cast<const float4*>(lbase + off); };
         nx = ldl(nb + sxo); fx = ldl(nb + (16u - sxo)); ny = ldl(nb + (32u + syo)); fy = ldl(nb + (48u - syo));
         nz = ldl(nb + (64u + szo)); fz = ldl(nb + (80u - szo));
         it = *reinterpret_cast<const uint4*>(lbase + (nb + 96u));
-#endif
       } else {
         const char* const nbase = reinterpret_cast<const char*>(sc.nodes);
         auto ldn = [&](uint32_t off) { return *reinterpret_cast<const float4*>(nbase + off); };
         nx = ldn(nb + sxo); fx = ldn(nb + (16u - sxo)); ny = ldn(nb + (32u + syo)); fy = ldn(nb + (48u - syo));
         nz = ldn(nb + (64u + szo)); fz = ldn(nb + (80u - szo));
         it = *reinterpret_cast<const uint4*>(nbase + (nb + 96u));
-#if !defined(RTG_HOST_EMU) && !defined(RTG_LATE_ITEMS)
+#if !defined(RTG_HOST_EMU)
         asm volatile("" ::"v"(it.x), "v"(it.y), "v"(it.z), "v"(it.w));   // as above
 #endif
       }
-#ifdef RTG_EXTRA_LOAD   // diagnostic: one more 16-B load per node step (the node's unused last row)
-      { const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.nodes) + nb + 112u);
-        asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w)); }
-#endif
-#ifdef RTG_STAMP
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#if RTG_PK_SLAB && !defined(RTG_HOST_EMU)
-      // the 24 plane distances two children at a time: v_pk_add_f32 (with
-      // the origin negated and broadcast) + v_pk_mul_f32, the same IEEE
-      // operations per lane as the scalar form below, so t0..t3 are
-      // bit-identical; half the VALU issue of the slab arithmetic
-      typedef float pf2 __attribute__((ext_vector_type(2)));
-      auto pk = [](float a, float b) { pf2 r = {a, b}; return r; };
-      const pf2 ox = pk(T.cr.o.x, T.cr.o.x), oy = pk(T.cr.o.y, T.cr.o.y), oz = pk(T.cr.o.z, T.cr.o.z);
-      const pf2 ix = pk(T.cr.inv.x, T.cr.inv.x), iy = pk(T.cr.inv.y, T.cr.inv.y), iz = pk(T.cr.inv.z, T.cr.inv.z);
-      const pf2 nx01 = (pk(nx.x, nx.y) - ox) * ix, nx23 = (pk(nx.z, nx.w) - ox) * ix;
-      const pf2 fx01 = (pk(fx.x, fx.y) - ox) * ix, fx23 = (pk(fx.z, fx.w) - ox) * ix;
-      const pf2 ny01 = (pk(ny.x, ny.y) - oy) * iy, ny23 = (pk(ny.z, ny.w) - oy) * iy;
-      const pf2 fy01 = (pk(fy.x, fy.y) - oy) * iy, fy23 = (pk(fy.z, fy.w) - oy) * iy;
-      const pf2 nz01 = (pk(nz.x, nz.y) - oz) * iz, nz23 = (pk(nz.z, nz.w) - oz) * iz;
-      const pf2 fz01 = (pk(fz.x, fz.y) - oz) * iz, fz23 = (pk(fz.z, fz.w) - oz) * iz;
-      t0 = slab(nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x);
-      t1 = slab(nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y);
-      t2 = slab(nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x);
-      t3 = slab(nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y);
-#else
       auto child_t = [&](float nxp, float fxp, float nyp, float fyp, float nzp, float fzp) {
         return slab((nxp - T.cr.o.x) * T.cr.inv.x, (fxp - T.cr.o.x) * T.cr.inv.x, (nyp - T.cr.o.y) * T.cr.inv.y,
                     (fyp - T.cr.o.y) * T.cr.inv.y, (nzp - T.cr.o.z) * T.cr.inv.z, (fzp - T.cr.o.z) * T.cr.inv.z);
@@ -1264,22 +1120,8 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       t1 = child_t(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y);
       t2 = child_t(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z);
       t3 = child_t(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w);
-#endif
     }
     if (kCount) cnt.nodes++;
-#ifdef RTG_EXTRA_VALU   // diagnostic: RTG_EXTRA_VALU more VALU per node step (four independent chains)
-    {
-      float x0 = t0, x1 = t1, x2 = t2, x3 = t3;
-      for (int k = 0; k < RTG_EXTRA_VALU / 4; ++k) {
-        x0 = fmaf(x0, 1.0001f, 0.5f); x1 = fmaf(x1, 1.0001f, 0.5f);
-        x2 = fmaf(x2, 1.0001f, 0.5f); x3 = fmaf(x3, 1.0001f, 0.5f);
-      }
-      asm volatile("" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3));
-    }
-#endif
-#ifdef RTG_STAMP
-    const uint32_t st1 = rtg_stamp();
-#endif
     // near-to-far order (5-comparator network, missed children sort last as
     // +inf); visit the nearest, push the other hit children far first
     uint32_t i0 = it.x, i1 = it.y, i2 = it.z, i3 = it.w;
@@ -1288,22 +1130,9 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
       const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
     };
-    // (any-hit rays: RTG_ANY_NOSORT skips the sort, the first hit child in
-    // slot order is visited first; an unoccluded ray visits every child it
-    // enters whatever the order)
-    if (!exact && !(kAny && RTG_ANY_NOSORT)) { cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2); }
-    if (kAny && RTG_ANY_NOSORT) {
-      // the first hit child (slot order) into slot 0; the others are pushed
-      auto mv = [](float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
-        const bool sw = !(ta < __builtin_inff()) && tb < __builtin_inff();
-        const float t = sw ? tb : ta; tb = sw ? ta : tb; ta = t;
-        const uint32_t i = sw ? ib : ia; ib = sw ? ia : ib; ia = i;
-      };
-      mv(t0, i0, t1, i1); mv(t0, i0, t2, i2); mv(t0, i0, t3, i3);
-    }
-#ifdef RTG_STAMP
-    const uint32_t st2 = rtg_stamp();
-#endif
+    // (any-hit rays sort too: visiting the first hit child in slot order
+    // instead measured C4 2151 / 2158 against 2159 / 2161 Msamples/s)
+    if (!exact) { cs(t0, i0, t1, i1); cs(t2, i2, t3, i3); cs(t0, i0, t2, i2); cs(t1, i1, t3, i3); cs(t1, i1, t2, i2); }
     if (exact) {
       // reference order: the hit children pushed right to left with their
       // entry distances, the leftmost popped (and so visited) first
@@ -1329,25 +1158,11 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE && T.lf == ITEM_NONE) postpone();
-#ifdef RTG_STAMP
-    if (st_lead) {
-      const uint32_t st3 = rtg_stamp();
-      cnt.st_load += st1 - st0; cnt.st_math += st2 - st1; cnt.st_rest += st3 - st2; cnt.st_steps++;
-    }
-#endif
     // leave phase 1 once at most kP1Slack lanes lack a postponed item
-    if (__popcll(__ballot(T.lf == ITEM_NONE)) <= (kVol ? kP1SlackVol : kAny ? kP1SlackAny : kP1Slack)) break;
+    if (__popcll(__ballot(T.lf == ITEM_NONE)) <= (kVol ? kP1SlackVol : kP1Slack)) break;
   }
   // ---------------- phase 2: leaves, instance entry / exit
-#ifdef RTG_STAMP
-  const bool st_lead2 = rtg_lead();
-  const uint32_t st4 = rtg_stamp();
-#endif
   while (T.lf != ITEM_NONE) {
-#ifdef RTG_STAMP
-    const bool st_l = rtg_lead();
-    const uint32_t sa = rtg_stamp();
-#endif
     uint32_t tag = T.lf >> ITEM_SHIFT, idx = T.lf & ITEM_MASK;
     if (kWide && tag == ITEM_LREF) {   // a leaf of a non-triangle 8-wide node: its item first
       T.lf = sc.litems[GIX(idx, sc.n_litems, 63)];
@@ -1524,9 +1339,6 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
     } else {  // ITEM_INST_END: back to the world-space ray
       T.cr = S.world_ray(); S.set_cur_ref(-1);
     }
-#ifdef RTG_STAMP
-    const uint32_t sb = rtg_stamp();
-#endif
     T.lf = ITEM_NONE;
     // ITEM_NONE here only means the stack was empty when this lane last
     // popped; the leaf just processed may have pushed instance items since.
@@ -1537,23 +1349,7 @@ __device__ __forceinline__ int trav_step(const DScene& sc, Trav& T, const TStack
       T.item = pop();
     }
     if (T.item != ITEM_NONE && (T.item >> ITEM_SHIFT) != ITEM_NODE) postpone();
-#ifdef RTG_STAMP
-    if (st_l) {
-      const uint32_t se = rtg_stamp();
-      const uint32_t body = sb - sa;
-      if (tag == ITEM_INSTANCE || tag == ITEM_WINST) cnt.st_inst += body;
-      else if (tag == ITEM_INST_END) cnt.st_end += body;
-      else cnt.st_leaf += body;
-      cnt.st_tail += se - sb; cnt.st_rounds++;
-    }
-#endif
-    // leave phase 2 once at most kP2Slack lanes would process another item
-    // (they keep it postponed for the next round)
-    if (kP2Slack > 0 && __popcll(__ballot(T.lf != ITEM_NONE)) <= kP2Slack) break;
   }
-#ifdef RTG_STAMP
-  if (st_lead2) cnt.st_p2 += rtg_stamp() - st4;
-#endif
   return (T.item == ITEM_NONE && T.lf == ITEM_NONE) ? TRAV_DONE : TRAV_RUNNING;
 }
 
@@ -1601,14 +1397,6 @@ __device__ __forceinline__ void set_face(V3 d, V3 outward, Rec& rec) {
   rec.N = rec.front ? outward : neg(outward);
 }
 
-// RTG_TRI_SHADE: a winning triangle's vertex, edges, normal and material
-// come from its 64-B DTriShade record (one request) instead of the 36-B
-// DTri (which straddles two lines 27 % of the time) plus the 16-B DTriAux.
-// CornellBoxLucy: k_shade 9.03 -> 8.78 ms per launch, its HBM-side traffic
-// over its algorithmic bytes 1.163 -> 1.062, frame bit-identical.
-#ifndef RTG_TRI_SHADE
-#define RTG_TRI_SHADE 1
-#endif
 // kUV = false: the scene has no ImageTexture (sc.needs_uv is 0), so the U/V
 // code is compiled out instead of branched over.
 template <bool kUV = true>
@@ -1672,19 +1460,13 @@ __device__ Rec make_record(const DScene& sc, const Best& b, V3 wo, V3 wd, float 
       rec.v = (dot(lp, bv) / ci.r + 1.0f) * 0.5f;
     }
   } else {  // PK_TRI
-#if RTG_TRI_SHADE
-    // one 64-B record: vertex, edges, normal, material (DTriShade)
+    // one 64-B record: vertex, edges, normal, material (DTriShade: k_shade
+    // 9.03 -> 8.78 ms per launch on C4 against the 36-B DTri, which
+    // straddles two lines 27 % of the time, plus a 16-B normal record)
     const DTriShade& ts = sc.tri_shade[GIX(b.idx, sc.n_tris, 24)];
     set_face(d, mk(ts.nx, ts.ny, ts.nz), rec);
     rec.mat = ts.mat;
     const V3 v0 = ld3(ts.v0), e1 = ld3(ts.e1), e2 = ld3(ts.e2);
-#else
-    const DTriAux& ax = sc.tri_aux[GIX(b.idx, sc.n_tris, 24)];
-    set_face(d, mk(ax.nx, ax.ny, ax.nz), rec);
-    rec.mat = ax.mat;
-    const DTri& tr = sc.tris[GIX(b.idx, sc.n_tris, 36)];
-    const V3 v0 = ld3(tr.v0), e1 = ld3(tr.e1), e2 = ld3(tr.e2);
-#endif
     // Moller-Trumbore (u, v) of the winner (triangle.go:57-101).  The hit
     // point is v0 + u*e1 + v*e2: equal to r.At(t) (triangle.go:97) to ~1e-13
     // in the reference's float64, but in fp32 it lies on the triangle's plane
@@ -1859,12 +1641,7 @@ __device__ __forceinline__ V3 disk_point(uint32_t key) {   // RandomInUnitDisk (
 // Inlined: as a call it made the bounce-0 kernels save their live registers
 // around the call site (k_extend<kFirst> 22 VGPRs spilled, 320 B of scratch
 // per lane; inlined 8 and 36 B): CornellBoxLucy 1970 -> 2008 Msamples/s.
-#ifdef RTG_NOINLINE_SLOW_CAMERA
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-void get_ray_slow(const DCamera& cam, int px, int py, uint32_t key, float offx, float offy,
+__device__ __forceinline__ void get_ray_slow(const DCamera& cam, int px, int py, uint32_t key, float offx, float offy,
                                           float time, V3& ro, V3& rd) {
   V3 center = add(ld3(cam.c_orig), scale(ld3(cam.c_dir), time));          // centerMotion.At(rayTime)
   V3 w;

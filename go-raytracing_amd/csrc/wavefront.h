@@ -46,22 +46,30 @@ struct WaveArgs {
   unsigned long long* counters;
   int* err;
   int32_t refill;   // lanes per wave lacking a prefetched item that trigger a claim
-  uint32_t* spill;  // traversal-stack spill area: spill_cap entries x spill_lanes
+  uint32_t* spill;  // traversal-stack spill area: spill_cap entries x spill_lanes (k_extend, k_tail)
+  uint32_t* spill_sh;   // k_shadow's (its own area when it overlaps the next k_extend: WavePlan::overlap)
   uint32_t spill_lanes;
   int32_t spill_cap;
   uint32_t slots;   // capacity of every per-slot array (RTG_GUARD bounds checks)
   uint32_t out_pixels;  // pixels of the output frame (RTG_GUARD: k_finalize's scattered store)
-  int32_t keep_vis;     // k_shadow stores the visibility words even when it applies the NEE itself (path probes)
 };
 
 // Queue counters, each on its own 128-B line (same-line atomics serialise);
 // the claim counters are 8 each, one per queue segment / XCD (wavefront.hip
-// pool_take, shade_claim), 32 words apart.
-enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT = 96, CNT_FETCH_SH = 352,
-             CNT_SHADE_SEG = 608, CNT_WORDS_Q = 864 };
+// pool_take, shade_claim), 32 words apart.  The NEE job count and k_shadow's
+// claim counters come in two sets, by bounce parity: bounce b's k_shadow /
+// k_nee_apply may still run while bounce b + 1's k_extend (which zeroes the
+// set of bounce b + 1) runs (WavePlan::overlap).
+enum : int { CNT_STREAM0 = 0, CNT_STREAM1 = 32, CNT_SHADOW = 64, CNT_FETCH_EXT = 128, CNT_FETCH_SH = 384,
+             CNT_SHADE_SEG = 896, CNT_WORDS_Q = 1152 };
+__host__ __device__ constexpr int cnt_shadow(int parity) { return CNT_SHADOW + 32 * parity; }
+__host__ __device__ constexpr int cnt_fetch_sh(int parity) { return CNT_FETCH_SH + 256 * parity; }
 
-// Traversal kernels: LDS stack ring of kLdsStack entries per lane, the rest
-// of the depth (up to kStackMax) spills to global memory.
+// Traversal kernels: an LDS stack ring of kLdsStack entries per lane, the
+// rest of the depth (up to kStackMax) spills to global memory.  (A 16-entry
+// ring at 6 waves per SIMD measured 745 against 757 Msamples/s for 8 entries
+// at 7 waves, round 1.)
+constexpr int kLdsStack = 8;
 // 128 covers the 8-wide format's bound (flatten.h kStackMax8; BVH4 scenes
 // need at most 64, the probe kernels' LDS stack).
 constexpr int kStackMax = 128;
@@ -83,15 +91,19 @@ struct WavePlan {
   int32_t max_blocks;       // > 0: cap on the persistent traversal grids (RT_OPT_MAX_BLOCKS)
   int32_t debug_sync;       // RTGPU_DEBUG_SYNC=1: synchronise after every launch, name a failing kernel
   int32_t num_twins;        // 1..kMaxTwins parts of the pixel list on their own streams (run_batches)
+  // Bounce overlap (scenes with lights): twin t's k_shadow / k_nee_apply of
+  // bounce b run on aux[t] while its k_extend of bounce b + 1 runs on its own
+  // stream; ev_shade[t] / ev_nee[t] order them (run_batches).
+  int32_t overlap;
+  const hipStream_t* aux;
+  const hipEvent_t* ev_shade;
+  const hipEvent_t* ev_nee;
   uint32_t* probe_host;     // pinned words (one per twin) for the long-tail early exit
   int* bounces_run;         // out (may be null): bounces the last batch ran (< max_depth after the early exit)
   // Per-launch timing (rt_set_kernel_timing): events 2k and 2k+1 are
   // recorded before and after one extend / shade / shadow launch on its
   // stream; ev_class[2k] names the kernel (low 4 bits, KC_*) and the twin
   // that launched it (bits 4-5).
-  // twin phase offset (RT_OPT_TWIN_OFFSET): twin 1 starts once twin 0's
-  // first k_extend has finished, so the twins run different kernels at a time
-  hipEvent_t offset_ev;     // nullptr: no offset
   hipEvent_t* events;       // nullptr: timing off
   uint8_t* ev_class;
   int max_events;
@@ -111,6 +123,6 @@ hipError_t guard_report(unsigned int out[4]);   // diagnostic build: first bad i
 #endif
 // as[t] / sts[t] for t < plan.num_twins: each twin's buffers and stream.
 hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
-                            const WavePlan& plan, int stack, bool count, float* out, int accumulate);
+                            const WavePlan& plan, bool count, float* out, int accumulate);
 
 }  // namespace rtg

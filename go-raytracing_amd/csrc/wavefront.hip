@@ -21,63 +21,35 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
-#ifdef RTG_WAVETIME
-#include <algorithm>
-#include <vector>
-#endif
+#include <type_traits>
 
 #include "dev_layout.h"
 #include "device_common.h"
 #include "wavefront.h"
 
+namespace rtg {
+
 // Minimum waves per SIMD requested for the traversal kernels (register cap:
 // 7 waves = 72 VGPRs).  The traversal is latency- and issue-bound, so
 // occupancy pays; measured on CornellBoxLucy (Msamples/s): 5 waves / 16-entry
-// LDS ring 681, 6 / 16 745, 7 / 8 757, 8 / 8 756 (64 B/lane of spills).  The
-// 8-entry ring + world ray + hit record (21.5 KB per block in k_extend) lets
-// LDS hold the 7 blocks per CU that 7 waves/SIMD need.
-#ifndef RTG_TRAV_WAVES
-#define RTG_TRAV_WAVES 7
-#endif
-// The volume (fog) and instrumented variants carry more live state: at the
-// 96-VGPR cap they spill 40-120 VGPRs to scratch, so they keep 4 waves
-// (128 VGPRs) and compile without VGPR spills.
-#ifndef RTG_VOL_WAVES
-#define RTG_VOL_WAVES 4
-#endif
-#define RTG_TRAV_WAVES_FOR(kVol, kCount) ((kCount) ? 4 : (kVol) ? RTG_VOL_WAVES : RTG_TRAV_WAVES)
-// any-hit shadow traversal carries no hit record: its own occupancy knob
-#ifndef RTG_SHADOW_WAVES
-#define RTG_SHADOW_WAVES RTG_TRAV_WAVES
-#endif
-#define RTG_SHADOW_WAVES_FOR(kVol, kCount) ((kCount) ? 4 : (kVol) ? RTG_VOL_WAVES : RTG_SHADOW_WAVES)
+// LDS ring 681, 6 / 16 745, 7 / 8 757, 8 / 8 756 (64 B/lane of spills); the
+// any-hit kernel at 6 or 8 waves was slower than at 7 too.  The volume (fog)
+// and instrumented variants carry more live state: at the 96-VGPR cap they
+// spill 40-120 VGPRs, so they keep 4 waves (128 VGPRs) and no spills.
+constexpr int kTravWaves = 7, kVolWaves = 4;
+#define TRAV_WAVES(kVol, kCount) ((kCount) ? 4 : (kVol) ? kVolWaves : kTravWaves)
 // BVH4 nodes held in LDS per block (trav_step kLdsN; fp32 node format only),
 // in what the LDS leaves beside the stack ring at 7 waves per SIMD (160 KB
 // per CU, allocated in 512-B granules: at most 45 granules, 23040 B, per
 // block).  k_shadow: 16 words per lane (the world ray's 1/d recomputed on
-// instance exit) + 48 nodes = 22 KB.  k_extend keeps the 1/d in LDS
-// (RTG_EXT_WINV: 22 words per lane, room for 4 nodes, the top of the world
-// BVH): recomputing it there cost 4 % of its single-stream time, more than
-// 28 LDS nodes returned (DESIGN §3 "LDS node cache").
-#ifndef RTG_EXT_WINV
-#define RTG_EXT_WINV 1
-#endif
-#ifndef RTG_LDS_NODES_EXT
-#define RTG_LDS_NODES_EXT (RTG_EXT_WINV ? 4 : 28)
-#endif
-#ifndef RTG_FIRST_NOINV
-#define RTG_FIRST_NOINV 0
-#endif
-#ifndef RTG_LDS_NODES_SH
-#define RTG_LDS_NODES_SH 48
-#endif
-#ifndef RTG_LDS_NODES_TAIL
-#define RTG_LDS_NODES_TAIL 64
-#endif
-#define RTG_LDS_N(k, kQuant, kWide) (((kQuant) || (kWide)) ? 0 : (k))
-#define RTG_LDS_ARR(k) ((k) > 0 ? (k) * 8 : 1)
-
-namespace rtg {
+// instance exit) + 48 nodes = 22 KB.  k_extend keeps the 1/d in LDS (22
+// words per lane, room for 4 nodes, the top of the world BVH): recomputing it
+// there to make room for 28 nodes cost 4 % of its single-stream time, more
+// than the nodes returned (DESIGN §3 "LDS node cache").  k_tail (4 waves)
+// keeps the 1/d and 64 nodes.
+constexpr int kLdsNodesExt = 4, kLdsNodesSh = 48, kLdsNodesTail = 64;
+constexpr int lds_nodes_for(int k, bool kQuant, bool kWide) { return (kQuant || kWide) ? 0 : k; }
+constexpr int lds_node_rows(int k) { return k > 0 ? k * 8 : 1; }
 
 __device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t asu(float f) { return __float_as_uint(f); }
@@ -128,18 +100,6 @@ __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n
   atomicAdd(c + 11, (unsigned long long)n.env);
   atomicAdd(c + 12, (unsigned long long)n.ibox);
   atomicAdd(c + 13, (unsigned long long)n.spill);
-#ifdef RTG_STAMP
-  atomicAdd(c + 16, (unsigned long long)n.st_load);
-  atomicAdd(c + 17, (unsigned long long)n.st_math);
-  atomicAdd(c + 18, (unsigned long long)n.st_rest);
-  atomicAdd(c + 19, (unsigned long long)n.st_p2);
-  atomicAdd(c + 20, (unsigned long long)n.st_steps);
-  atomicAdd(c + 21, (unsigned long long)n.st_leaf);
-  atomicAdd(c + 22, (unsigned long long)n.st_inst);
-  atomicAdd(c + 23, (unsigned long long)n.st_end);
-  atomicAdd(c + 15, (unsigned long long)n.st_tail);
-  atomicAdd(c + 14, (unsigned long long)n.st_rounds);
-#endif
 }
 
 // ---------------------------------------------------------------- camera
@@ -170,36 +130,11 @@ __device__ __forceinline__ void camera_ray(const DCamera& cam, const WaveArgs& a
 // its 4-MB L2 holds the part of the scene those rays touch.  Each segment has
 // its own claim counter (its own 128-B line).  Which wave traces a ray never
 // changes the ray's result.
-#ifndef RTG_TAIL_NO_PREFETCH
-#define RTG_TAIL_NO_PREFETCH 1
-#endif
-#ifndef RTG_NO_PREFETCH
-#define RTG_NO_PREFETCH 0   // diagnostic: lanes claim only when idle (no prefetched next ray)
-#endif
-#ifndef RTG_XCD_SEGMENTS
-#define RTG_XCD_SEGMENTS 1
-#endif
-// claim runs are 1/(RTG_GSS_DIV x waves per segment) of what a wave last
-// saw left in its segment
-#ifndef RTG_GSS_LAG
-#define RTG_GSS_LAG 0
-#endif
-#ifndef RTG_GSS_DIV
-#define RTG_GSS_DIV 4
-#endif
-// long-tail scenes: the traversal grids follow the rays left (run_batches)
-#ifndef RTG_TAIL_GRID
-#define RTG_TAIL_GRID 1
-#endif
-// NEE contributions added by k_shadow with no-return float atomics (scenes
-// without HDRI importance sampling): no k_nee_apply launch.  Bit-identical
-// frames, but measured much slower (C4 2029 -> 1811 Msamples/s, k_shadow
-// 52.4 -> 89.9 ms per frame against k_nee_apply's 11.7: three scattered
-// float atomics per visible job, each a line fetched into L2 and modified
-// there, plus 35 VGPRs spilled at the 72 cap); a diagnostic variant
-#ifndef RTG_NEE_ATOMIC
-#define RTG_NEE_ATOMIC 0
-#endif
+// Claim runs are 1/(kGssDiv x waves per segment) of what a wave last saw
+// left in its segment.  (Sizing them from the counter's extrapolated
+// position, a fixed first run, or finer bounce-0 runs all measured no
+// better: DESIGN §6.)
+constexpr uint32_t kGssDiv = 4;
 constexpr uint32_t kSegs = 8;
 constexpr uint32_t kSegStride = 32;   // words between the segment counters
 struct Pool {
@@ -208,11 +143,6 @@ struct Pool {
   uint32_t tried;      // segments found drained
   bool dry;            // every segment is drained
   bool tail;           // the queue is nearly drained (runs at their minimum): stop prefetching
-  uint32_t lag;        // RTG_GSS_LAG: how far the counter moved while the wave traced its last run
-#ifdef RTG_WAVETIME
-  uint32_t nclaims = 0, lastrun = 0, steals = 0;   // diagnostic: the wave's claims, its last run, its steal claims
-  unsigned long long tlast = 0;                    // diagnostic: wall clock of the last claim
-#endif
 };
 __device__ __forceinline__ uint32_t xcc_id() {
 #ifdef RTG_HOST_EMU
@@ -224,15 +154,9 @@ __device__ __forceinline__ uint32_t xcc_id() {
 #endif
 }
 __device__ __forceinline__ Pool pool_init() {
-#if RTG_XCD_SEGMENTS
   Pool P{};
-  P.cur = 0u; P.end = 0u; P.seg = xcc_id(); P.tried = 0u; P.dry = false; P.tail = false; P.lag = 0u;
+  P.cur = 0u; P.end = 0u; P.seg = xcc_id(); P.tried = 0u; P.dry = false; P.tail = false;
   return P;
-#else
-  Pool P{};
-  P.cur = 0u; P.end = 0u; P.seg = 0u; P.tried = 0u; P.dry = false; P.tail = false; P.lag = 0u;
-  return P;
-#endif
 }
 
 // Called by the whole wave (converged).  Lanes with `want` get a queue
@@ -247,8 +171,8 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   if (P.cur >= P.end) {
     // (in the tail any idle lane claims: there is no later batch to wait for)
     if (nw < uint32_t(P.tail ? 1 : refill)) return ITEM_NONE;
-    const uint32_t segs = RTG_XCD_SEGMENTS ? kSegs : 1u;
-    const uint32_t wps = RTG_XCD_SEGMENTS ? (nwaves + kSegs - 1u) / kSegs : nwaves;   // waves per segment
+    const uint32_t segs = kSegs;
+    const uint32_t wps = (nwaves + kSegs - 1u) / kSegs;   // waves per segment
     const int leader = __ffsll(m) - 1;
     for (;;) {
       const uint32_t lo = uint32_t((uint64_t(n) * P.seg) / segs), hi = uint32_t((uint64_t(n) * (P.seg + 1u)) / segs);
@@ -258,35 +182,19 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
       // start, as an own-segment claim is, a late steal took up to 1/(4 wps)
       // of a whole segment — dozens of rays per lane, traced after every
       // other wave had finished.
-      uint32_t run = P.tried ? 0u : (hi - from) / (uint32_t(RTG_GSS_DIV) * wps);
+      uint32_t run = P.tried ? 0u : (hi - from) / (kGssDiv * wps);
       // in a segment's last 256 rays per wave a lane stops holding a
       // prefetched ray behind its current one: a ray left queued behind
       // another lane's long traversal would end the kernel that much later
-      P.tail = RTG_NO_PREFETCH || (RTG_TAIL_NO_PREFETCH && run < 64u);
-#if RTG_GSS_LAG
-      // the run sized from the counter's extrapolated position: the wave's
-      // own last run end plus what the others claimed while it traced that
-      // run (a wave back from a long run would otherwise size its claim from
-      // a stale position and take a large run near the segment's end)
-      if (!P.tried) {
-        const uint32_t fx = hi - from > P.lag ? from + P.lag : hi;
-        run = (hi - fx) / (uint32_t(RTG_GSS_DIV) * wps);
-      }
-#endif
+      P.tail = run < 64u;
       run = run < 64u ? 64u : (run > 4096u ? 4096u : run);
       uint32_t base = 0;
       if (__lane_id() == leader) base = atomicAdd(ctr + P.seg * kSegStride, run);
       // wave-uniform: scalar registers for the pool state
       base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + lo;
       if (base < hi) {
-#if RTG_GSS_LAG
-        P.lag = (!P.tried && P.end > lo && P.end <= hi && base > P.end) ? base - P.end : 0u;
-#endif
         P.cur = base;
         P.end = hi - base > run ? base + run : hi;
-#ifdef RTG_WAVETIME
-        P.nclaims++; P.lastrun = P.end - P.cur; P.tlast = wall_clock64(); P.steals += P.tried ? 1u : 0u;
-#endif
         break;
       }
       // this segment is drained: the next one (a wave every segment's
@@ -304,50 +212,11 @@ __device__ __forceinline__ uint32_t pool_take(bool want, Pool& P, uint32_t* ctr,
   return idx;
 }
 
-#ifdef RTG_WAVETIME
-// Diagnostic builds only: per wave of the last traversal launch, its start
-// and end on the 100 MHz wall clock and the rays it traced (run_batches
-// prints the distribution after each launch).  Vector stores from lane 0.
-constexpr int kWtWaves = 16384;
-constexpr int kWtWords = 6;
-__device__ unsigned long long rtg_wt[kWtWords * kWtWaves];
-__device__ __forceinline__ void wavetime_note(unsigned long long t0, uint32_t rays, const Pool& P) {
-  const unsigned long long t1 = wall_clock64();
-  for (int o = 32; o > 0; o >>= 1) rays += __shfl_xor(rays, o);
-  const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (__lane_id() == 0 && w < uint32_t(kWtWaves)) {
-    unsigned long long* r = rtg_wt + size_t(kWtWords) * w;
-    r[0] = t0;
-    r[1] = t1;
-    r[2] = rays;
-    r[3] = P.nclaims | (uint64_t(P.steals) << 32);
-    r[4] = P.tlast;
-    r[5] = P.lastrun;
-  }
-}
-#endif
-
-// Result stores (hit records, visibility words) through L2 (temporal), so a
-// wave's lanes finishing at different steps fill whole lines there before
-// they are written back, instead of one partial-line write each (VERDICT r4
-// #4: WRITE_SIZE 2.2x / 8x the record bytes with non-temporal stores)
-#ifndef RTG_RESULT_TEMPORAL
-#define RTG_RESULT_TEMPORAL 0
-#endif
-template <typename V>
-__device__ __forceinline__ void st_result(V* p, V v) {
-  if (RTG_RESULT_TEMPORAL) *p = v;
-  else stnt(p, v);
-}
 __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_t p, Best b) {
   resolve_inst(sc, b);
   const float4 r = make_float4(b.t, asf(b.kind ? ((uint32_t(b.kind) << 28) | uint32_t(b.idx)) : 0u), asf(uint32_t(b.inst)),
                                asf(uint32_t(b.refpos)));
-#ifdef RTG_DIAG_NO_RESULT_STORES
-  // diagnostic bound only (wrong frames): the store kept but never taken
-  if (__float_as_uint(r.x) == 0x7FC00123u)
-#endif
-  st_result(&hit[p], r);
+  stnt(&hit[p], r);
 }
 
 // ---------------------------------------------------------------- extend
@@ -357,18 +226,17 @@ __device__ __forceinline__ void store_hit(const DScene& sc, float4* hit, uint32_
 // kFirst: bounce 0, the rays are the camera rays of the claimed slots (the
 // prefetch loads only the slot's pixel; GetRay runs when the ray starts).
 template <int STACK, bool kCount, bool kVol, bool kFirst, bool kQuant = false, bool kWide = false>
-__global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_extend(DScene sc, DCamera cam, WaveArgs a,
+static __global__ __launch_bounds__(256, TRAV_WAVES(kVol, kCount)) void k_extend(DScene sc, DCamera cam, WaveArgs a,
                                                                 PathStream cs, const uint32_t* count,
                                                                 uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
                                                                 uint32_t* fetch, uint32_t sample_base) {
-  // RTG_FIRST_NOINV: bounce 0's camera rays recompute the world 1/d and take
-  // 28 LDS nodes (A/B knob)
-  constexpr bool kWinv = RTG_EXT_WINV != 0 && !(kFirst && RTG_FIRST_NOINV);
-  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + (kWinv ? kWorldInvWords : 0) + kHitWords) * 256];   // stack ring + world ray + hit record
-  constexpr int kLds = RTG_LDS_N(kWinv ? RTG_LDS_NODES_EXT : 28, kQuant, kWide);
-  __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
+  __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kWorldInvWords + kHitWords) * 256];   // stack ring + world ray + hit record
+  constexpr int kLds = lds_nodes_for(kLdsNodesExt, kQuant, kWide);
+  __shared__ float4 lds_nodes[lds_node_rows(kLds)];
   lds_nodes_fill<kLds>(sc, lds_nodes);
-  // next stream's count, the shadow job count and the shadow fetch counter
+  // next stream's count, this bounce's NEE job count and k_shadow claim
+  // counters (their parity set, cnt_shadow / cnt_fetch_sh: the previous
+  // bounce's k_shadow may still be claiming from the other set)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *zero_a = 0u;
     *zero_b = 0u;
@@ -384,25 +252,18 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
   if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(60, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
 #endif
   const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
-                 a.spill_cap, lds_nodes, kWinv};
+                 a.spill_cap, lds_nodes, true};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
   Pool P = pool_init();
   uint32_t p = ITEM_NONE, pn = ITEM_NONE;
   float4 po = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pd = po;
   uint32_t pb = 0;
-#ifdef RTG_WAVETIME
-  const unsigned long long wt0 = wall_clock64();
-  uint32_t wt_rays = 0;
-#endif
   for (;;) {
     if (p == ITEM_NONE && pn != ITEM_NONE) {
       p = pn;
       pn = ITEM_NONE;
       if (kCount) cnt.rays++;
-#ifdef RTG_WAVETIME
-      wt_rays++;
-#endif
       if (kFirst) {
         V3 ro, rd;
         uint32_t key;
@@ -416,7 +277,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE && (p == ITEM_NONE || !P.tail), P, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
-      pn = GIX(((RTG_CLAIM_PERM & (kFirst ? 1 : 4)) != 0) ? claim_perm(idx, n) : idx, a.slots, 40);
+      pn = GIX(idx, a.slots, 40);
       if (kFirst) {
         po.x = asf(slot_pixel(a, pn));   // the ray itself is made when it starts
       } else {
@@ -434,14 +295,7 @@ __global__ __launch_bounds__(256, RTG_TRAV_WAVES_FOR(kVol, kCount)) void k_exten
       if (s != TRAV_RUNNING) { store_hit(sc, a.hit, p, trav_best(T, S)); p = ITEM_NONE; }
     }
   }
-#ifdef RTG_WAVETIME
-  wavetime_note(wt0, wt_rays, P);
-#endif
-#ifdef RTG_STAMP
-  add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
-#else
   if (kCount) add_counters(a.counters + KC_EXTEND * CNT_BLOCK, cnt, 0);
-#endif
 }
 
 // ---------------------------------------------------------------- shade
@@ -471,9 +325,6 @@ __device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, u
 // the stream its XCD's k_extend waves traced (pool_take), then from the
 // others: the hit -> triangle / instance reads of shading then find the
 // records the same XCD's L2 just served to the traversal.
-#ifndef RTG_SHADE_SEGMENTS
-#define RTG_SHADE_SEGMENTS 1
-#endif
 __device__ __forceinline__ uint32_t shade_claim(uint32_t* ctr, uint32_t nchunks, uint32_t& seg, uint32_t& tried) {
   for (;;) {
     const uint32_t lo = uint32_t((uint64_t(nchunks) * seg) / kSegs), hi = uint32_t((uint64_t(nchunks) * (seg + 1u)) / kSegs);
@@ -514,12 +365,10 @@ __device__ __forceinline__ void shade_path(const DScene& sc, const DCamera& cam,
   uint32_t kh = asu(h.y);
   float ht = h.x;
   int hinst = int(asu(h.z));
-#ifndef RTG_DIAG_NO_VOL   // diagnostic builds only: the shading kernel without its volume tests (wrong frames)
   if (kShade == SHADE_VOL) {
     int hrefpos = int(asu(h.w));
     lifted_volumes<kCount>(sc, ro, rd, key, bounce, kh, ht, hinst, hrefpos, cnt, vrecs);
   }
-#endif
 #ifdef RTG_GUARD
   if (kh == 0xFFFFFFFFu) rtg_guard_note(50, slot, bounce);   // hit record never written by k_extend
 #endif
@@ -652,11 +501,7 @@ __device__ __forceinline__ void shade_path(const DScene& sc, const DCamera& cam,
             }
           }
         }
-#ifdef RTG_DIAG_NO_VOL
-        if (false) {
-#else
         if (kShade == SHADE_VOL && flags != 0u) {
-#endif
           // a lifted volume occluding a shadow ray (camera.go:582, :639;
           // the any-hit traversal's volume test, same interval and RNG
           // domain) clears the ray: its contribution is not applied
@@ -699,58 +544,29 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
                               : 0;
 }
 
-// k_shade at 4 waves per SIMD (128 VGPRs, 2 of them spilled): CornellBoxLucy
-// 1749 -> 1783 Msamples/s against the compiler's own choice (130 VGPRs, 3
-// waves); the shading loop waits on its dependent hit -> triangle / instance
-// reads, so occupancy pays once the spill cost is this small.
-#ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 4
-#endif
-// The lean variant (kFancy false: Lambertian / DiffuseLight with solid or
-// checker textures, no U/V code) needs 87-93 VGPRs without spills; 5 waves
-// is also the most its LDS tables (31.5 KB per block) allow.  CornellBoxLucy
-// 1835 (all variants at 4 waves, 128 VGPRs, 2 spilled) -> 1871 (lean at 4)
-// -> 1874 Msamples/s (lean at 5), bit-identical frames.  With its LDS tables
-// sized to the scene (shade_lds_bytes) the lean variant runs at 7 waves (72
-// VGPRs, 4 spilled): 1896 (5) / 1934 (6) / 1978 (7) / 1928 (8 waves): a
-// 72-VGPR block also fits beside the traversal kernels' 72-VGPR waves when
-// the twin streams overlap them.
-#ifndef RTG_SHADE_LEAN_WAVES
-#define RTG_SHADE_LEAN_WAVES 7
-#endif
-// The middle variant (Metal / Dielectric / Isotropic, solid or checker
-// textures: C2, C3, C5) at 7 waves (72 VGPRs, spilling): measured (4 / 5 /
-// 6 / 7 waves) C2 3473 / 3502 / 3473 / 3632, C3 1014 / 1019 / 1022 / 1005,
-// C5 8548 / 8684 / 8751 / 8973 Msamples/s (the full variant at 4 waves:
-// C2 3376, C3 1013, C5 8216).
-#ifndef RTG_SHADE_MAT_WAVES
-#define RTG_SHADE_MAT_WAVES 7
-#endif
-// The volume variant (the material one + the lifted volumes' tests): C3
-// CornellBoxScene at 4 / 5 / 7 waves 1390 / 1454 / 1427 Msamples/s (110 / 96
-// / 72 VGPRs; 0 / 3 / 71 spilled); with the volume records (DVolRec, round
-// 4) 4 / 5 / 6 waves 1580 / 1648 / 1660 (101 / 96 / 80 VGPRs; 0 / 0 / 13
-// spilled); with the records read by scalar loads, 5 / 6 / 7 waves 1886 /
-// 1927 / 1928 (96 / 80 / 72 VGPRs; 0 / 16 / 53 spilled).
-#ifndef RTG_SHADE_VOL_WAVES
-#define RTG_SHADE_VOL_WAVES 6
-#endif
-#define RTG_SHADE_WAVES_FOR(kShade)                                                       \
-  ((kShade) == SHADE_FULL ? RTG_SHADE_WAVES : (kShade) == SHADE_MAT ? RTG_SHADE_MAT_WAVES \
-   : (kShade) == SHADE_VOL ? RTG_SHADE_VOL_WAVES : RTG_SHADE_LEAN_WAVES)
-// bounce 0's variants (camera ray generation inlined) may take their own
-// occupancy (RTG_SHADE_FIRST_WAVES > 0; A/B knob)
-#ifndef RTG_SHADE_FIRST_WAVES
-#define RTG_SHADE_FIRST_WAVES 0
-#endif
-#define RTG_SHADE_WAVES_FOR2(kShade, kFirst) \
-  ((kFirst) && RTG_SHADE_FIRST_WAVES > 0 ? RTG_SHADE_FIRST_WAVES : RTG_SHADE_WAVES_FOR(kShade))
+// k_shade occupancy per variant (waves per SIMD):
+//   full (Noise / Image textures): 4 (128 VGPRs; 5 and 6 waves spill 38 and
+//     105 VGPRs: C2 3130 / 3119 / 3078, C5 7625 / 7605 / 7389 Msamples/s);
+//   lean (Lambertian / DiffuseLight, solid or checker): 7 (72 VGPRs, 4
+//     spilled; C4 1896 / 1934 / 1978 / 1928 at 5 / 6 / 7 / 8 waves: a
+//     72-VGPR block fits beside the traversal kernels' 72-VGPR waves when the
+//     twin streams overlap them; its LDS tables are sized to the scene);
+//   material (+ Metal / Dielectric / Isotropic: C2, C3, C5): 7 (C2 3473 /
+//     3502 / 3473 / 3632, C5 8548 / 8684 / 8751 / 8973 at 4 / 5 / 6 / 7);
+//   volume (+ the lifted volumes' tests: C3): 6 (records read by scalar
+//     loads; 5 / 6 / 7 waves 1886 / 1927 / 1928 at 96 / 80 / 72 VGPRs, 0 /
+//     16 / 53 spilled).
+// A separate occupancy for bounce 0's variants (6 / 5 waves) was no faster.
+constexpr int kShadeFullWaves = 4, kShadeLeanWaves = 7, kShadeMatWaves = 7, kShadeVolWaves = 6;
+#define SHADE_WAVES(kShade)                                                     \
+  ((kShade) == SHADE_FULL ? kShadeFullWaves : (kShade) == SHADE_MAT ? kShadeMatWaves \
+   : (kShade) == SHADE_VOL ? kShadeVolWaves : kShadeLeanWaves)
 // kFirst: bounce 0 — the path is the slot's camera ray (no stream to read)
 // and this kernel initialises the slot's radiance in Lout.
 template <bool kCount, bool kEnvIS, int kShade, bool kFirst>
-__global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                const uint32_t* count, PathStream ns, uint32_t* ncount,
-                                               uint32_t sample_base) {
+                                               uint32_t* jcount, uint32_t sample_base) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
   // sit on every path's dependent-load chain (hit -> material -> texture,
   // light -> light material -> texture).
@@ -786,16 +602,16 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
   }
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
-  // without lights no k_shadow runs (run_batches): reset the next extend's
-  // fetch counter here (this extend has finished claiming)
-  if (sc.num_lights == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+  // reset the next extend's claim counters here: this bounce's k_extend has
+  // finished claiming, and the next one starts after this kernel (k_shadow
+  // may run beside the next k_extend, WavePlan::overlap)
+  if (blockIdx.x == 0 && threadIdx.x == 0)
     for (uint32_t k = 0; k < kSegs; ++k) a.counts[CNT_FETCH_EXT + k * kSegStride] = 0u;
   Cnt cnt = {};
   // block-uniform trip count (blockDim 256, gs a multiple of 256): every
   // thread reaches the block_reserve2 barriers
   const uint32_t n_up = (n + 255u) & ~255u;
   uint32_t par = 0;
-#if RTG_SHADE_SEGMENTS
   (void)gs;
   __shared__ uint32_t s_chunk[2];   // double-buffered like s_w / s_b
   uint32_t seg = xcc_id(), tried = 0;
@@ -805,9 +621,6 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
     const uint32_t chunk = s_chunk[par];
     if (chunk == 0xFFFFFFFFu) break;   // block-uniform
     const uint32_t i = chunk * blockDim.x + threadIdx.x;
-#else
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += gs, par ^= 1u) {
-#endif
     const bool live = i < n;
     bool cont = false, want_shadow = false;
     uint32_t slot = 0, key = 0, flags = 0, bounce = 0, nstate = 0;
@@ -846,7 +659,7 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
     }
     if (kFirst && live && !lout_set) stnt(&a.Lout[GIX(slot, a.slots, 44)], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     uint32_t jc = 0, js = 0;
-    block_reserve2(cont, want_shadow, ncount, a.counts + CNT_SHADOW, s_w[par], s_b[par], jc, js);
+    block_reserve2(cont, want_shadow, ncount, jcount, s_w[par], s_b[par], jc, js);
     if (cont) {
       jc = GIX(jc, a.slots, 43);
       stnt(&ns.o[jc], make_float4(P.x, P.y, P.z, asf(slot)));
@@ -885,15 +698,13 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES_FOR2(kShade, kFirst)) void k_s
 // operations in the same order as in k_extend / k_shade (the same RNG keys,
 // the same Lout[slot] adds), so the frame is bit-identical.  Scenes with
 // lights keep the wavefront schedule: their NEE jobs need k_shadow.
-#ifndef RTG_TAIL_WAVES
-#define RTG_TAIL_WAVES 4
-#endif
+constexpr int kTailWaves = 4;
 template <int STACK, bool kVol, int kShade, bool kQuant, bool kWide>
-__global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
+static __global__ __launch_bounds__(256, kTailWaves) void k_tail(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                               const uint32_t* count, uint32_t* fetch) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords + kWorldInvWords + kHitWords) * 256];   // stack ring + world ray + hit record
-  constexpr int kLds = RTG_LDS_N(RTG_LDS_NODES_TAIL, kQuant, kWide);
-  __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
+  constexpr int kLds = lds_nodes_for(kLdsNodesTail, kQuant, kWide);
+  __shared__ float4 lds_nodes[lds_node_rows(kLds)];
 #ifdef RTG_HOST_EMU
   static char s_dyn[kLdsMaterials * sizeof(DMaterial) + kLdsTextures * sizeof(DTexture) + kLdsLights * sizeof(DLight)];
 #else
@@ -983,24 +794,26 @@ __global__ __launch_bounds__(256, RTG_TAIL_WAVES) void k_tail(DScene scg, DCamer
 // contributions in that order, camera.go:549-558).  Lanes prefetch their next
 // job as k_extend does.
 template <int STACK, bool kCount, bool kVol, bool kEnvIS, bool kQuant = false, bool kWide = false>
-__global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
-                                                                uint32_t* fetch, uint32_t* zero_c) {
-  // RTG_NEE_ATOMIC: without HDRI importance sampling (an area-light ray per
-  // job) the visible contribution is added to Lout here and no k_nee_apply
-  // runs (run_batches)
-  constexpr bool kNeeAtomic = RTG_NEE_ATOMIC && !kEnvIS;
+static __global__ __launch_bounds__(256, TRAV_WAVES(kVol, kCount)) void k_shadow(DScene sc, WaveArgs a, const uint32_t* count,
+                                                                uint32_t* fetch, uint32_t* zero_next) {
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
-  constexpr int kLds = RTG_LDS_N(RTG_LDS_NODES_SH, kQuant, kWide);
-  __shared__ float4 lds_nodes[RTG_LDS_ARR(kLds)];
+  constexpr int kLds = lds_nodes_for(kLdsNodesSh, kQuant, kWide);
+  __shared__ float4 lds_nodes[lds_node_rows(kLds)];
   lds_nodes_fill<kLds>(sc, lds_nodes);
-  if (blockIdx.x == 0 && threadIdx.x == 0)   // next extend's segment counters
-    for (uint32_t k = 0; k < kSegs; ++k) zero_c[k * kSegStride] = 0u;
+  // the next bounce's claim counters (the other parity set, cnt_fetch_sh:
+  // the k_shadow that used it last ran before this one on this stream).  The
+  // next k_extend zeroes them as well; this second reset is kept because the
+  // kernel's register allocation at the 72-VGPR cap depends on it: without
+  // it the production k_shadow spills 25 VGPRs instead of 7 (C4 2150 -> 2040
+  // Msamples/s)
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (uint32_t k = 0; k < kSegs; ++k) zero_next[k * kSegStride] = 0u;
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
 #ifdef RTG_GUARD
   if (threadIdx.x == 0 && (blockIdx.x + 1u) * blockDim.x > a.spill_lanes) rtg_guard_note(61, (blockIdx.x + 1u) * blockDim.x, a.spill_lanes);
 #endif
-  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
+  const TStack S{lds_stack + threadIdx.x, 256, STACK, a.spill_sh + blockIdx.x * blockDim.x, lds_stack, int(a.spill_lanes),
                  a.spill_cap, lds_nodes};
   Cnt cnt = {};
   Trav T{};   // fully initialised: no undef state flows through the divergent loop
@@ -1013,7 +826,6 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
   float4 da = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   // prefetched job
   float4 qp = da, qa = da, qh = da;
-  float4 qe = da;   // kNeeAtomic: the job's contribution (x beta) and path slot (ne_a)
   uint32_t qinfo = 1u;
   auto start_ray = [&](int rr, V3 dir, float tmax) -> int {
     if (kCount) cnt.shadow++;
@@ -1031,24 +843,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       if (s2 == TRAV_RUNNING) return false;
       if (s2 != TRAV_ANYHIT) vis |= 1u;
     }
-    // (the words k_nee_apply reads; with kNeeAtomic only the path probe
-    // reads them: a 4-B scattered store per job saved)
-#ifdef RTG_DIAG_NO_RESULT_STORES
-    if (vis == 0xDEADu)
-#endif
-    if (!kNeeAtomic || a.keep_vis) st_result(&a.sj_vis[p], vis);
-    if (kNeeAtomic && (vis & 1u)) {
-      // k_nee_apply's L + contribution, here: one float add per component in
-      // the L2 atomic unit, with no return (the lane does not wait).  Within
-      // a bounce this is the only update of Lout[slot] (one NEE job per
-      // path; k_shade's adds are in the kernels before and after), so the
-      // sum is k_nee_apply's, bit for bit.  da holds ne_a once the job's
-      // area ray has started (see the job start below).
-      float* Lp = &a.Lout[GIX(asu(da.w), a.slots, 47)].x;
-      atomicAddNoRet(Lp, da.x);
-      atomicAddNoRet(Lp + 1, da.y);
-      atomicAddNoRet(Lp + 2, da.z);
-    }
+    stnt(&a.sj_vis[p], vis);   // the word k_nee_apply reads
     return true;
   };
   for (;;) {
@@ -1068,17 +863,15 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
         r = 1;
         s = start_ray(1, mk(da.x, da.y, da.z), da.w);               // camera.go:639
       }
-      if (kNeeAtomic) da = qe;   // the area direction is dead once its ray started (no HDRI ray follows)
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
     const uint32_t idx = pool_take(pn == ITEM_NONE && (p == ITEM_NONE || !Q.tail), Q, fetch, n, nwaves, a.refill);
     if (idx != ITEM_NONE) {
-      pn = GIX((RTG_CLAIM_PERM & 2) != 0 ? claim_perm(idx, n) : idx, a.slots, 46);
+      pn = GIX(claim_perm(idx, n), a.slots, 46);
       qp = ldnt(&a.sj_p[pn]);
       qa = ldnt(&a.sj_a[pn]);
       if (kEnvIS) qh = ldnt(&a.sj_h[pn]);
       if (kEnvIS || kVol) qinfo = ldnt(&a.sj_info[pn]);
-      if (kNeeAtomic) qe = ldnt(&a.ne_a[pn]);
     }
     if (!__any(p != ITEM_NONE || pn != ITEM_NONE)) {
       if (Q.dry) break;
@@ -1089,11 +882,7 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
       if (s != TRAV_RUNNING && advance(s)) p = ITEM_NONE;
     }
   }
-#ifdef RTG_STAMP
-  add_counters(a.counters + KC_SHADOW * CNT_BLOCK, cnt, 0);
-#else
   if (kCount) add_counters(a.counters + KC_SHADOW * CNT_BLOCK, cnt, 0);
-#endif
 }
 
 // ---------------------------------------------------------------- NEE apply
@@ -1101,29 +890,17 @@ __global__ __launch_bounds__(256, RTG_SHADOW_WAVES_FOR(kVol, kCount)) void k_sha
 // contribution if visible), summed in that order (camera.go:549-558).
 // Without HDRI importance sampling a job carries beta * contribution already;
 // a job whose rays were all occluded adds zero and is skipped.
-#ifndef RTG_NEE_EAGER
-#define RTG_NEE_EAGER 0
-#endif
 template <bool kEnvIS>
-__global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count) {
+static __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* count) {
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
     const uint32_t kk = GIX(k, a.slots, 59);
     // (k_shadow sets a visibility bit only for a ray the job asked for, so
     // the job's flag word need not be read: vis & flags == vis)
-#if RTG_NEE_EAGER
-    // the job's contribution read with its visibility word (one dependent
-    // round trip less before the Lout read-modify-write; an occluded job's
-    // 16 B are read for nothing)
-    const uint32_t vis = ldnt(&a.sj_vis[kk]);
-    const float4 ea = ldnt(&a.ne_a[kk]);
-    if ((vis & 3u) == 0u) continue;
-#else
     const uint32_t vis = ldnt(&a.sj_vis[kk]);
     if ((vis & 3u) == 0u) continue;
     const float4 ea = ldnt(&a.ne_a[kk]);
-#endif
     float4* Lp = a.Lout + GIX(asu(ea.w), a.slots, 47);
     const float4 L4 = ldnt(Lp);
     V3 L;
@@ -1141,7 +918,7 @@ __global__ __launch_bounds__(256) void k_nee_apply(WaveArgs a, const uint32_t* c
 }
 
 // ---------------------------------------------------------------- accumulate
-__global__ __launch_bounds__(256) void k_accum(WaveArgs a, uint32_t nsamp) {
+static __global__ __launch_bounds__(256) void k_accum(WaveArgs a, uint32_t nsamp) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x; pi < a.npix; pi += gs) {
     double sx = a.acc[size_t(pi) * 3], sy = a.acc[size_t(pi) * 3 + 1], sz = a.acc[size_t(pi) * 3 + 2];
@@ -1153,7 +930,7 @@ __global__ __launch_bounds__(256) void k_accum(WaveArgs a, uint32_t nsamp) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int accumulate) {
+static __global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int accumulate) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t pi = blockIdx.x * blockDim.x + threadIdx.x; pi < a.npix; pi += gs) {
     float* o = out + size_t(GIX(a.pixels[pi], a.out_pixels, 58)) * 3;
@@ -1163,18 +940,19 @@ __global__ __launch_bounds__(256) void k_finalize(WaveArgs a, float* out, int ac
   }
 }
 
-__global__ void k_set_counts(uint32_t* c, uint32_t n) {
+static __global__ void k_set_counts(uint32_t* c, uint32_t n) {
   if (threadIdx.x == 0) {
-    c[CNT_STREAM0] = n; c[CNT_STREAM1] = 0u; c[CNT_SHADOW] = 0u;
+    c[CNT_STREAM0] = n; c[CNT_STREAM1] = 0u; c[cnt_shadow(0)] = 0u; c[cnt_shadow(1)] = 0u;
     for (uint32_t k = 0; k < kSegs; ++k) {
       c[CNT_FETCH_EXT + k * kSegStride] = 0u;
-      c[CNT_FETCH_SH + k * kSegStride] = 0u;
+      c[cnt_fetch_sh(0) + k * kSegStride] = 0u;
+      c[cnt_fetch_sh(1) + k * kSegStride] = 0u;
       c[CNT_SHADE_SEG + k * kSegStride] = 0u;
     }
   }
 }
 
-__global__ void k_count_samples(WaveArgs a, uint32_t n) {
+static __global__ void k_count_samples(WaveArgs a, uint32_t n) {
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters, (unsigned long long)n);
 }
 
@@ -1222,62 +1000,6 @@ static hipError_t mark_end(const WavePlan& plan, hipStream_t st) {
     }                                                                                                  \
   } while (0)
 
-#ifdef RTG_WAVETIME
-// After a traversal launch (diagnostic builds): the waves' end times after
-// the first start, as percentiles, the last start, and the rays per wave.
-static hipError_t wavetime_report(const char* name, int bounce, int nwaves, hipStream_t st) {
-  hipError_t e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return e;
-  if (nwaves > kWtWaves) nwaves = kWtWaves;
-  std::vector<unsigned long long> h(size_t(kWtWords) * nwaves);
-  if ((e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rtg_wt), h.size() * sizeof(unsigned long long))) != hipSuccess) return e;
-  unsigned long long t0 = ~0ull, s_last = 0;
-  for (int w = 0; w < nwaves; ++w) t0 = std::min(t0, h[kWtWords * w]);
-  std::vector<double> ends(nwaves), rays(nwaves);
-  double tot = 0;
-  for (int w = 0; w < nwaves; ++w) {
-    ends[w] = double(h[kWtWords * w + 1] - t0) / 100.0;   // us
-    s_last = std::max(s_last, h[kWtWords * w] - t0);
-    rays[w] = double(h[kWtWords * w + 2]);
-    tot += rays[w];
-  }
-  {
-    // the last-ending 2 % of the waves against the rest: when they made their
-    // last claim, how big it was, how many claims and steals they made
-    std::vector<int> idx(nwaves);
-    for (int w = 0; w < nwaves; ++w) idx[w] = w;
-    std::sort(idx.begin(), idx.end(), [&](int x, int y) { return ends[x] < ends[y]; });
-    auto stats = [&](int from, int to, const char* tag) {
-      std::vector<double> lc, lr, nc, ns, gap;
-      for (int k = from; k < to; ++k) {
-        const int w = idx[k];
-        const unsigned long long* r = &h[size_t(kWtWords) * w];
-        lc.push_back(r[4] ? double(r[4] - t0) / 100.0 : 0.0);
-        lr.push_back(double(r[5]));
-        nc.push_back(double(r[3] & 0xFFFFFFFFull));
-        ns.push_back(double(r[3] >> 32));
-        gap.push_back(r[4] ? double(r[1] - r[4]) / 100.0 : 0.0);
-      }
-      auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
-      auto mx = [](const std::vector<double>& v) { return v.empty() ? 0.0 : *std::max_element(v.begin(), v.end()); };
-      fprintf(stderr, "RTG_WAVETIME   %s: last claim at med %.1f us, last run med %.0f max %.0f, claims med %.0f, steals med %.0f, last claim -> end med %.1f max %.1f us\n",
-              tag, med(lc), med(lr), mx(lr), med(nc), med(ns), med(gap), mx(gap));
-    };
-    const int cut = nwaves - std::max(1, nwaves / 50);
-    stats(0, cut, "first 98%");
-    stats(cut, nwaves, "last 2% ");
-  }
-  std::vector<double> se = ends, sr = rays;
-  std::sort(se.begin(), se.end());
-  std::sort(sr.begin(), sr.end());
-  auto pc = [&](const std::vector<double>& v, double q) { return v[size_t(q * (v.size() - 1))]; };
-  fprintf(stderr, "RTG_WAVETIME %s b%d waves %d rays %.0f | last start %.1f us | end p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us | rays/wave p10 %.0f p50 %.0f p99 %.0f\n",
-          name, bounce, nwaves, tot, double(s_last) / 100.0, pc(se, 0.1), pc(se, 0.5), pc(se, 0.9), pc(se, 0.99), se.back(),
-          pc(sr, 0.1), pc(sr, 0.5), pc(sr, 0.99));
-  return hipSuccess;
-}
-#endif
-
 // The render's work is split into twins (WavePlan::num_twins, 1 or 2):
 // disjoint halves of the pixel list, each with its own path slots, queue
 // counters, spill area and HIP stream, enqueued bounce by bounce in
@@ -1317,58 +1039,67 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
       gext[t] = cap(grid_for((const void*)k_extend<STACK, kCount, kVol, false, kQuant, kWide>, 256, 0, nslots, cus));
     }
     if (plan.bounces_run) *plan.bounces_run = 0;
+    // Bounce overlap (plan.overlap, scenes with lights): k_shadow and
+    // k_nee_apply of bounce b run on the twin's aux stream while its k_extend
+    // of bounce b + 1 (which needs only k_shade b's survivors) runs on its own
+    // stream; k_shade b + 1 waits for k_nee_apply b (both update Lout[slot],
+    // and k_shade b + 1 rewrites the NEE job arrays).  The two kernels that
+    // run together use their own spill areas and their own parity sets of
+    // the NEE counters (cnt_shadow, cnt_fetch_sh); k_shade resets the next
+    // k_extend's claim counters.  Each path sees the same operations in the
+    // same order, so the frame is bit-identical to the serial schedule.
+    const bool ovl = nee && plan.overlap != 0;
     for (int b = 0; b < plan.max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
       if (plan.bounces_run) *plan.bounces_run = b + 1;
       for (int t = 0; t < nt; ++t) {
         const WaveArgs& a = as[t];
         const hipStream_t st = sts[t];
+        const hipStream_t sx = ovl ? plan.aux[t] : st;   // k_shadow / k_nee_apply stream
         uint32_t* const cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
-        uint32_t* const cnt_shadow = a.counts + CNT_SHADOW;
+        uint32_t* const cnt_sh = a.counts + cnt_shadow(c);
         uint32_t* const fetch_ext = a.counts + CNT_FETCH_EXT;
-        uint32_t* const fetch_sh = a.counts + CNT_FETCH_SH;
+        uint32_t* const fetch_sh = a.counts + cnt_fetch_sh(c);
 #ifdef RTG_GUARD
         // poison the hit records: k_shade reports any that k_extend did not write
         if ((e = hipMemsetAsync(a.hit, 0xFF, size_t(a.slots) * sizeof(float4), st)) != hipSuccess) return e;
 #endif
         // bounce 0 regenerates the camera rays (no stream), later bounces read s[c]
-        const bool offset = plan.offset_ev && s0 == 0 && b == 0 && nt > 1;
-        if (offset && t == 1 && (e = hipStreamWaitEvent(st, plan.offset_ev, 0)) != hipSuccess) return e;
         if ((e = mark_begin(plan, uint8_t(KC_EXTEND | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, true, kQuant, kWide>), dim3(gext0[t]), dim3(256), 0, st, sc, cam, a,
-                             a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+                             a.s[c], cnt_stream[c], cnt_stream[nx], cnt_sh, fetch_sh, fetch_ext, sample_base);
         else
           hipLaunchKernelGGL((k_extend<STACK, kCount, kVol, false, kQuant, kWide>), dim3(gext[t]), dim3(256), 0, st, sc, cam, a,
-                             a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh, fetch_ext, sample_base);
+                             a.s[c], cnt_stream[c], cnt_stream[nx], cnt_sh, fetch_sh, fetch_ext, sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
-        if (offset && t == 0 && (e = hipEventRecord(plan.offset_ev, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_extend", b, st);
-#ifdef RTG_WAVETIME
-        if ((e = wavetime_report("k_extend", b, b == 0 ? gext0[t] * 4 : gext[t] * 4, st)) != hipSuccess) return e;
-#endif
+        // k_shade b waits for k_nee_apply b - 1
+        if (ovl && b > 0 && (e = hipStreamWaitEvent(st, plan.ev_nee[t], 0)) != hipSuccess) return e;
         if ((e = mark_begin(plan, uint8_t(KC_SHADE | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, true>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
-                             cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+                             cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, sample_base);
         else
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, false>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
-                             cnt_stream[c], a.s[nx], cnt_stream[nx], sample_base);
+                             cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, sample_base);
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_shade", b, st);
         // no lights: k_shade writes no NEE job (sampleLightMIS needs a light,
-        // camera.go:502), so the shadow and apply launches are skipped; k_shade
-        // then resets the next extend's fetch counter itself
+        // camera.go:502), so the shadow and apply launches are skipped
         if (nee) {
-          if ((e = mark_begin(plan, uint8_t(KC_SHADOW | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
-          hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant, kWide>), dim3(gsd[t]), dim3(256), 0, st, sc, a,
-                             cnt_shadow, fetch_sh, fetch_ext);
-          if ((e = mark_end(plan, st)) != hipSuccess) return e;
-          RTG_LAUNCHED("k_shadow", b, st);
-          if (kEnvIS || !RTG_NEE_ATOMIC) {   // (else k_shadow applied the contributions)
-            hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap[t]), dim3(256), 0, st, a, cnt_shadow);
-            RTG_LAUNCHED("k_nee_apply", b, st);
+          if (ovl) {
+            if ((e = hipEventRecord(plan.ev_shade[t], st)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(sx, plan.ev_shade[t], 0)) != hipSuccess) return e;
           }
+          if ((e = mark_begin(plan, uint8_t(KC_SHADOW | (t << KC_TWIN_SHIFT)), sx)) != hipSuccess) return e;
+          hipLaunchKernelGGL((k_shadow<STACK, kCount, kVol, kEnvIS, kQuant, kWide>), dim3(gsd[t]), dim3(256), 0, sx, sc, a,
+                             cnt_sh, fetch_sh, a.counts + cnt_fetch_sh(nx));
+          if ((e = mark_end(plan, sx)) != hipSuccess) return e;
+          RTG_LAUNCHED("k_shadow", b, sx);
+          hipLaunchKernelGGL(k_nee_apply<kEnvIS>, dim3(gap[t]), dim3(256), 0, sx, a, cnt_sh);
+          RTG_LAUNCHED("k_nee_apply", b, sx);
+          if (ovl && (e = hipEventRecord(plan.ev_nee[t], sx)) != hipSuccess) return e;
         }
       }
       if (plan.max_depth > 8 && ((b >= 7 && (b % 4) == 3) || (plan.tail_rays > 0 && b == plan.tail_first))) {
@@ -1384,7 +1115,6 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
           if ((e = hipStreamSynchronize(sts[t])) != hipSuccess) return e;
           left += plan.probe_host[t];
           lefts[t] = plan.probe_host[t];
-#if RTG_TAIL_GRID
           // the counts only shrink from here: size the persistent grids for
           // what is left (every wave of a launch makes at least one claim
           // atomic on eight counters, about 0.14 ms per launch at the full
@@ -1395,7 +1125,6 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
           if (g < gext[t]) gext[t] = g;
           if (g < gsd[t]) gsd[t] = g;
           if (g < gsh[t]) gsh[t] = g;   // k_shade: one 256-path chunk claim per block
-#endif
         }
         if (left == 0) break;
         // few paths left in a render without lights: one k_tail launch per
@@ -1417,6 +1146,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         }
       }
     }
+    // the twin's stream continues once its last k_nee_apply has finished
+    if (ovl)
+      for (int t = 0; t < nt; ++t)
+        if ((e = hipStreamWaitEvent(sts[t], plan.ev_nee[t], 0)) != hipSuccess) return e;
     if (!kCount)
       for (int t = 0; t < nt; ++t) {
         const hipStream_t st = sts[t];
@@ -1440,8 +1173,58 @@ hipError_t guard_report(unsigned int out[4]) {
 }
 #endif
 
+// The variants a scene's traversal and shading compile to: node format (RT_NODES_QUANT8 /
+// RT_NODES_WIDE8 scenes run their node format's own kernels: the default fp32 kernels carry
+// no trace of them; the 8-wide format has no rare-primitive variant, flatten builds it only
+// for scenes that do not need one), importance-sampled HDRI, shading kind.
+template <int S, bool C, bool V>
+static hipError_t run_variant(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
+                              const WavePlan& plan) {
+  // the importance-sampled HDRI is a NEE light only beside an area light
+  // (sampleLightMIS needs one, camera.go:502): without lights the kEnvIS code
+  // is dead, and its registers spilled (C5: 34 VGPRs in bounce 0's shading)
+  const bool envis = sc.env.valid && sc.env.use_is && sc.num_lights > 0;
+  const int shade = sc.shade_kind;
+  auto by_shade = [&](auto E, auto Q, auto W) {
+    constexpr bool kE = decltype(E)::value, kQ = decltype(Q)::value, kW = decltype(W)::value;
+    if (shade == SHADE_FULL) return run_batches<S, C, V, kE, SHADE_FULL, kQ, kW>(sc, cam, as, sts, plan);
+    if (shade == SHADE_VOL) return run_batches<S, C, V, kE, SHADE_VOL, kQ, kW>(sc, cam, as, sts, plan);
+    if (shade == SHADE_MAT) return run_batches<S, C, V, kE, SHADE_MAT, kQ, kW>(sc, cam, as, sts, plan);
+    return run_batches<S, C, V, kE, SHADE_LEAN, kQ, kW>(sc, cam, as, sts, plan);
+  };
+  auto by_env = [&](auto Q, auto W) {
+    return envis ? by_shade(std::true_type{}, Q, W) : by_shade(std::false_type{}, Q, W);
+  };
+  if constexpr (!V) {
+    if (sc.wide_nodes != 0) return by_env(std::false_type{}, std::true_type{});
+  }
+  if (sc.quant_nodes != 0) return by_env(std::true_type{}, std::false_type{});
+  return by_env(std::false_type{}, std::false_type{});
+}
+
+// Each variant group is instantiated in its own translation unit (compiled in
+// parallel): RTG_WF_GROUP 0 (this file: stack ring 8, plain kernels, and
+// launch_wavefront), 1 (wf_vol.hip: rare-primitive kernels), 2
+// (wf_count.hip: instrumented kernels).
+#ifndef RTG_WF_GROUP
+#define RTG_WF_GROUP 0
+#endif
+#if RTG_WF_GROUP == 1 && !defined(RTG_DIAG_RING)
+hipError_t run_group_vol8(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
+                          const WavePlan& plan) {
+  return run_variant<8, false, true>(sc, cam, as, sts, plan);
+}
+#elif RTG_WF_GROUP == 2 && !defined(RTG_DIAG_RING)
+hipError_t run_group_count8(bool vol, const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
+                            const WavePlan& plan) {
+  return vol ? run_variant<8, true, true>(sc, cam, as, sts, plan) : run_variant<8, true, false>(sc, cam, as, sts, plan);
+}
+#elif RTG_WF_GROUP == 0
+hipError_t run_group_vol8(const DScene&, const DCamera&, const WaveArgs*, const hipStream_t*, const WavePlan&);
+hipError_t run_group_count8(bool, const DScene&, const DCamera&, const WaveArgs*, const hipStream_t*, const WavePlan&);
+
 hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs* as, const hipStream_t* sts,
-                            const WavePlan& plan, int stack, bool count, float* out, int accumulate) {
+                            const WavePlan& plan, bool count, float* out, int accumulate) {
   hipError_t e;
   const int nt = plan.num_twins;
   for (int t = 0; t < nt; ++t)
@@ -1450,62 +1233,17 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
     // the kVol variants also carry the rare primitives (circles)
     // (and the reference-order closest hit of RotateX/Z scenes, DScene.dfs_order)
     const bool vol = sc.has_volumes != 0 || sc.n_circles > 0 || sc.dfs_order != 0;
-#define RUN3(S, C, V, E, Q, W)                                                          \
-  do {                                                                                  \
-    if (shade == SHADE_FULL) e = run_batches<S, C, V, E, SHADE_FULL, Q, W>(sc, cam, as, sts, plan);        \
-    else if (shade == SHADE_VOL) e = run_batches<S, C, V, E, SHADE_VOL, Q, W>(sc, cam, as, sts, plan);     \
-    else if (shade == SHADE_MAT) e = run_batches<S, C, V, E, SHADE_MAT, Q, W>(sc, cam, as, sts, plan);     \
-    else e = run_batches<S, C, V, E, SHADE_LEAN, Q, W>(sc, cam, as, sts, plan);                            \
-  } while (0)
-#define RUN2(S, C, V, Q, W)               \
-  do {                                    \
-    if (envis) RUN3(S, C, V, true, Q, W); \
-    else RUN3(S, C, V, false, Q, W);      \
-  } while (0)
-    // RT_NODES_QUANT8 / RT_NODES_WIDE8 scenes run their node format's
-    // traversal (kernels of their own: the default fp32 kernels carry no
-    // trace of them); the 8-wide format has no rare-primitive variant
-    // (flatten builds it only for scenes that do not need one)
-#define RUN(S, C, V)                                                 \
-  do {                                                               \
-    if constexpr (!(V)) {                                            \
-      if (wide) { RUN2(S, C, V, false, true); break; }               \
-    }                                                                \
-    if (quant) RUN2(S, C, V, true, false);                           \
-    else RUN2(S, C, V, false, false);                                \
-  } while (0)
-    // the importance-sampled HDRI is a NEE light only beside an area light
-    // (sampleLightMIS needs one, camera.go:502): without lights the kEnvIS
-    // code is dead, and its registers spilled (C5: 34 VGPRs in bounce 0's
-    // shading)
-    const bool envis = sc.env.valid && sc.env.use_is && sc.num_lights > 0, quant = sc.quant_nodes != 0,
-               wide = sc.wide_nodes != 0;
-    const int shade = sc.shade_kind;
-#if defined(RTG_RING24) && !defined(RTG_DIAG_RING)
-#define RTG_DIAG_RING 24
-#endif
 #ifdef RTG_DIAG_RING
-    // diagnostic builds only (RTG_GUARD / RTG_RING24 bisection):
-    // one ring size for every scene, fp32 nodes, no counting variant (a
-    // short compile)
-    (void)quant;
-    (void)stack;
+    // diagnostic builds only (RTG_GUARD): one ring size for every
+    // scene, no counting variant (a short compile)
     if (count) return hipErrorNotSupported;
-    if (vol) RUN2(RTG_DIAG_RING, false, true, false, false);
-    else if (wide) RUN2(RTG_DIAG_RING, false, false, false, true);
-    else RUN2(RTG_DIAG_RING, false, false, false, false);
+    e = vol ? run_variant<RTG_DIAG_RING, false, true>(sc, cam, as, sts, plan)
+            : run_variant<RTG_DIAG_RING, false, false>(sc, cam, as, sts, plan);
 #else
-    if (stack > 8) {
-      if (vol) { if (count) RUN(16, true, true); else RUN(16, false, true); }
-      else { if (count) RUN(16, true, false); else RUN(16, false, false); }
-    } else {
-      if (vol) { if (count) RUN(8, true, true); else RUN(8, false, true); }
-      else { if (count) RUN(8, true, false); else RUN(8, false, false); }
-    }
+    if (count) e = run_group_count8(vol, sc, cam, as, sts, plan);
+    else if (vol) e = run_group_vol8(sc, cam, as, sts, plan);
+    else e = run_variant<8, false, false>(sc, cam, as, sts, plan);
 #endif
-#undef RUN
-#undef RUN2
-#undef RUN3
     if (e != hipSuccess) return e;
   }
   if (!count)
@@ -1514,6 +1252,7 @@ hipError_t launch_wavefront(const DScene& sc, const DCamera& cam, const WaveArgs
                          dim3(256), 0, sts[t], as[t], out, accumulate);
   return hipGetLastError();
 }
+#endif  // RTG_WF_GROUP
 #endif  // RTG_HOST_EMU
 
 }  // namespace rtg

@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the RT_ABI_VERSION this binding was written against.
-const ABIVersion = 7 // RT_ABI_VERSION
+const ABIVersion = 8 // RT_ABI_VERSION
 
 // Hittable kinds (enum rt_hittable_kind).
 const (
@@ -108,6 +108,7 @@ const (
 	OptDealing      int32 = 10 // RT_OPT_DEALING
 	OptDealFirst    int32 = 11 // RT_OPT_DEAL_FIRST
 	OptTail         int32 = 12 // RT_OPT_TAIL
+	OptOverlap      int32 = 13 // RT_OPT_OVERLAP
 	DealStatic      int32 = 0  // RT_DEAL_STATIC
 	DealDynamic     int32 = 1  // RT_DEAL_DYNAMIC
 )

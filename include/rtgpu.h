@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------ */
 enum rt_status {
@@ -361,13 +361,21 @@ int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t ma
  *     left, one persistent launch carries each of them through all its
  *     remaining bounces (closest hit and shading in one lane) instead of
  *     two launches per bounce.  Same operations per path in the same order:
- *     the frame is bit-identical.  0 (default) = automatic (2^20 paths), 1 =
- *     off (every bounce through the per-bounce kernels), n > 1 = threshold
- *     of n paths.                                                        */
+ *     the frame is bit-identical.  0 (default) = automatic (2^23 paths,
+ *     wavefront.h kTailRaysDefault), 1 = off (every bounce through the
+ *     per-bounce kernels), n > 1 = threshold of n paths.
+ *   RT_OPT_OVERLAP: in scenes with lights, bounce b's shadow rays
+ *     (k_shadow) and their NEE adds (k_nee_apply) run on a second stream
+ *     per part while bounce b + 1's closest-hit kernel (k_extend) runs, its
+ *     only input being bounce b's scattered rays (the reference's worker
+ *     carries one sample through every bounce, bucket_renderer.go:257-301,
+ *     camera.go:443-518).  Same operations per path in the same order: the
+ *     frame is bit-identical.  0 (default) = automatic (on, at most two
+ *     parts), 1 = off, 2 = on.                                           */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7,
        RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9, RT_OPT_DEALING = 10, RT_OPT_DEAL_FIRST = 11,
-       RT_OPT_TAIL = 12 };
+       RT_OPT_TAIL = 12, RT_OPT_OVERLAP = 13 };
 enum { RT_DEAL_STATIC = 0, RT_DEAL_DYNAMIC = 1 };
 enum { RT_BLAS_REFERENCE = 0, RT_BLAS_SAH = 1, RT_BLAS_DEVICE = 2 };
 enum { RT_NODES_FP32 = 0, RT_NODES_QUANT8 = 1, RT_NODES_WIDE8 = 2 };

@@ -71,7 +71,6 @@ int main(int argc, char** argv) {
   a.spill_cap = kStackMax - kRing;
   a.slots = 1;
   a.out_pixels = 1;
-  a.keep_vis = 1;
   float o[3], dd[3];
   while (scanf("%f %f %f %f %f %f", &o[0], &o[1], &o[2], &dd[0], &dd[1], &dd[2]) == 6) {
     const float4 ro{o[0], o[1], o[2], 0.0f}, rd{dd[0], dd[1], dd[2], 0.0f};

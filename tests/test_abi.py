@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol(g, header, lib):
 
 
 def test_abi_version(g):
-    assert g.rtgpu().rt_abi_version() == 7
+    assert g.rtgpu().rt_abi_version() == 8
 
 
 def test_no_silent_cpu_fallback_without_gpu(g):

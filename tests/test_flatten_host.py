@@ -194,6 +194,33 @@ def test_tail_kernel_bit_identical(wave, tmp_path, name, tail_after, nodes):
     assert np.array_equal(outs["wave"], outs["tail"])
 
 
+@pytest.mark.parametrize("name,batch,nodes", [("cornell-lucy", 1, "0"), ("cornell", 0, "0"), ("hdri-nee", 0, "0"),
+                                              ("cornell-smoke", 1, "1"), ("cornell-lucy", 0, "2"),
+                                              ("cornell-rotations", 0, "0")])
+def test_bounce_overlap_bit_identical(wave, tmp_path, name, batch, nodes):
+    """The bounce overlap (RT_OPT_OVERLAP: bounce b's k_shadow / k_nee_apply
+    beside bounce b + 1's k_extend) under ASan/UBSan, in the order that
+    separates them most (k_extend b + 1 runs to its end first): the NEE
+    counters of the two bounces are disjoint parity sets and k_shade resets
+    the claim counters, so the frame equals the serial schedule's bit for
+    bit, over several batches and every node format."""
+    spp, seed, width = 2, 11, 40
+    outs = {}
+    for mode in ("serial", "overlap"):
+        out = tmp_path / f"{name}_{mode}.f32"
+        env = _env()
+        env["RTG_EMU_QUANT"] = nodes
+        env["RTG_EMU_OVERLAP"] = "1" if mode == "overlap" else "0"
+        args = [wave, name, str(width), str(spp), str(seed), ASSETS, str(out)]
+        if batch:
+            args.append(str(batch))
+        r = subprocess.run(args, capture_output=True, text=True, env=env, timeout=600)
+        assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+        outs[mode] = np.fromfile(out, np.float32)
+    assert outs["serial"].sum() > 0
+    assert np.array_equal(outs["serial"], outs["overlap"])
+
+
 def test_grazing_sliver_ray_documented(tmp_path, g, O):
     """DESIGN.md §5 "Topology and grazing hits": the one C4 camera ray in
     95.9 M path rays (tools/oracle_ray_scan.py) on which the GPU's hit

@@ -27,30 +27,41 @@ constexpr int kRing = 4;
 template <bool kVol, bool kEnvIS, int kShade, bool kQuant, bool kWide = false>
 void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_t spb, int max_depth, float* out) {
   uint32_t* cnt_stream[2] = {a.counts + CNT_STREAM0, a.counts + CNT_STREAM1};
-  uint32_t* cnt_shadow = a.counts + CNT_SHADOW;
   uint32_t* fetch_ext = a.counts + CNT_FETCH_EXT;
-  uint32_t* fetch_sh = a.counts + CNT_FETCH_SH;
   for (double* p = a.acc; p < a.acc + size_t(a.npix) * 3; ++p) *p = 0.0;
   const int tail_after = getenv("RTG_EMU_TAIL") ? atoi(getenv("RTG_EMU_TAIL")) : -1;
+  // RTG_EMU_OVERLAP=1: the bounce overlap's order (run_batches, WavePlan::
+  // overlap): bounce b's k_shadow / k_nee_apply only after bounce b + 1's
+  // k_extend has run to its end, the most any interleaving of the two streams
+  // can separate them
+  const bool ovl = getenv("RTG_EMU_OVERLAP") && atoi(getenv("RTG_EMU_OVERLAP")) > 0;
+  auto nee = [&](int b) {   // as run_batches: no lights, no NEE launches
+    if (sc.num_lights == 0) return;
+    uint32_t* const cnt_sh = a.counts + cnt_shadow(b & 1);
+    k_shadow<kRing, false, kVol, kEnvIS, kQuant, kWide>(sc, a, cnt_sh, a.counts + cnt_fetch_sh(b & 1),
+                                                        a.counts + cnt_fetch_sh((b + 1) & 1));
+    k_nee_apply<kEnvIS>(a, cnt_sh);
+  };
   for (uint32_t s0 = 0; s0 < spp; s0 += spb) {
     const uint32_t sb = spp - s0 < spb ? spp - s0 : spb;
     const uint32_t nslots = sb * a.npix;
     k_set_counts(a.counts, nslots);
+    int pending = -1;   // the bounce whose NEE kernels have not run yet (ovl)
     for (int b = 0; b < max_depth; ++b) {
       const int c = b & 1, nx = c ^ 1;
-      if (b == 0) {
-        k_extend<kRing, false, kVol, true, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
-                                           fetch_ext, s0);
-        k_shade<false, kEnvIS, kShade, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
-      } else {
-        k_extend<kRing, false, kVol, false, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_shadow, fetch_sh,
-                                            fetch_ext, s0);
-        k_shade<false, kEnvIS, kShade, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], s0);
-      }
-      if (sc.num_lights > 0) {   // as run_batches: no lights, no NEE launches
-        k_shadow<kRing, false, kVol, kEnvIS, kQuant, kWide>(sc, a, cnt_shadow, fetch_sh, fetch_ext);
-        if (kEnvIS || !RTG_NEE_ATOMIC) k_nee_apply<kEnvIS>(a, cnt_shadow);   // as run_batches
-      }
+      uint32_t* const cnt_sh = a.counts + cnt_shadow(c);
+      uint32_t* const fetch_sh = a.counts + cnt_fetch_sh(c);
+      if (b == 0)
+        k_extend<kRing, false, kVol, true, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_sh, fetch_sh,
+                                                          fetch_ext, s0);
+      else
+        k_extend<kRing, false, kVol, false, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_sh, fetch_sh,
+                                                           fetch_ext, s0);
+      if (pending >= 0) { nee(pending); pending = -1; }
+      if (b == 0) k_shade<false, kEnvIS, kShade, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, s0);
+      else k_shade<false, kEnvIS, kShade, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, s0);
+      if (ovl) pending = b;
+      else nee(b);
       // RTG_EMU_TAIL=b: after bounce b the long-tail kernel carries every
       // path left to its end (run_batches' hand-off, scenes without lights)
       if (sc.num_lights == 0 && tail_after >= 0 && b == tail_after && b + 1 < max_depth) {
@@ -58,6 +69,7 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
         break;
       }
     }
+    if (pending >= 0) nee(pending);
     k_accum(a, sb);
   }
   k_finalize(a, out, 0);
@@ -85,7 +97,7 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> pixels(npix);
   // bucket-like pixel list: reversed, so slot -> pixel is not the identity
   for (uint32_t i = 0; i < npix; ++i) pixels[i] = npix - 1u - i;
-  std::vector<uint32_t> spill(size_t(kStackMax - kRing), 0u);
+  std::vector<uint32_t> spill(size_t(kStackMax - kRing), 0u), spill_sh(size_t(kStackMax - kRing), 0u);
   std::vector<double> acc(size_t(npix) * 3, 0.0);
   std::vector<unsigned long long> counters(3 * CNT_BLOCK, 0ull);
   int err = 0;
@@ -108,11 +120,11 @@ int main(int argc, char** argv) {
   a.err = &err;
   a.refill = 1;                      // one lane per wave: claim whenever idle
   a.spill = spill.data();
+  a.spill_sh = spill_sh.data();
   a.spill_lanes = 1;
   a.spill_cap = kStackMax - kRing;
   a.slots = uint32_t(S);
   a.out_pixels = uint32_t(npix);
-  a.keep_vis = 1;
 
   std::vector<float> out(size_t(npix) * 3, 0.0f);
   const bool vol = d.has_volumes != 0 || d.n_circles > 0 || d.dfs_order != 0, envis = d.env.valid && d.env.use_is;
