@@ -128,6 +128,17 @@ PMC_PASSES = [
              "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU"]),
 ]
 PMC_FAMILIES = ("k_extend", "k_shade", "k_shadow", "k_nee_apply", "k_accum", "k_finalize")
+# Bytes per FETCH_SIZE byte, per kernel family: calibrated on gfx950 by
+# tools/fetch_calib.sh (profiles/r06_fetch_calib.json).  Microkernels that miss
+# a known number of 128-B lines once each show one 64-B-tallied read request
+# per missed line for every access width: whole coalesced lines (128 B read:
+# 64.2 / 66.2 FETCH_SIZE bytes per line, factor 1.97), one 16-B row per line,
+# and k_extend's node step (7 of a line's 8 rows, both 64-B halves: still one
+# request per line, so the L2 fills whole 128-B lines).  On the bench
+# workload every production kernel's requests are of that class (0 % 32-B,
+# <= 0.03 % 128-B requests; 64.0 FETCH_SIZE bytes per request): x 2 for all.
+FETCH_FACTOR = {"extend": 2.0, "shade": 2.0, "shadow": 2.0, "nee_apply": 2.0, "accum": 2.0, "finalize": 2.0}
+FETCH_CALIBRATION = "profiles/r06_fetch_calib.json (tools/fetch_calib.sh)"
 
 
 def pmc_family(name: str):
@@ -138,8 +149,8 @@ def pmc_family(name: str):
 
 
 def run_pmc_passes(args) -> dict | None:
-    """Per kernel family and launch: HBM-side bytes (FETCH_SIZE x 2 per the
-    guide's gfx950 note + WRITE_SIZE, KiB counters), L2 hit rate, average
+    """Per kernel family and launch: HBM-side bytes (FETCH_SIZE x the family's
+    calibrated FETCH_FACTOR + WRITE_SIZE, KiB counters), L2 hit rate, average
     L2 read latency, wave wait share and VALU lane utilisation."""
     import csv
     import glob
@@ -184,12 +195,13 @@ def run_pmc_passes(args) -> dict | None:
             return v[c] / max(len(disp[fam][c]), 1)
         e = {"dispatches": max((len(s) for s in disp[fam].values()), default=0)}
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            fetch, write = per("FETCH_SIZE") * 1024 * 2, per("WRITE_SIZE") * 1024
+            ff = FETCH_FACTOR.get(fam, 2.0)
+            fetch, write = per("FETCH_SIZE") * 1024 * ff, per("WRITE_SIZE") * 1024
             # per dispatch, and over the profiled step (one step: with twin
             # streams a kernel's launch is two dispatches, kernel_report)
             e.update(fetch_bytes_per_launch=int(fetch), write_bytes_per_launch=int(write),
                      hbm_bytes_per_launch=int(fetch + write),
-                     hbm_bytes_step=int(v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024))
+                     hbm_bytes_step=int(v["FETCH_SIZE"] * 1024 * ff + v["WRITE_SIZE"] * 1024), fetch_factor=ff)
         h, m = v.get("TCC_HIT_sum", 0.0), v.get("TCC_MISS_sum", 0.0)
         if h + m > 0:
             e["l2_hit"] = round(h / (h + m), 4)
@@ -621,7 +633,7 @@ def main():
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
         kd = kernels[dom]
         # The bound: bytes the dominant kernel moves between L2 and the fabric
-        # (FETCH_SIZE x 2 + WRITE_SIZE per launch; Infinity-Cache hits are
+        # (FETCH_SIZE x its calibrated factor + WRITE_SIZE per launch; Infinity-Cache hits are
         # counted, so the DRAM share is lower still) over its launch time,
         # against the 8 TB/s HBM peak.  The algorithm's requested bytes
         #  are reported beside it: they exceed what the
@@ -630,7 +642,8 @@ def main():
         req_step_GBs = alg_step / (ms_per_step / 1e3) / 1e9
         roofline = {"bound": "hbm", "achieved": kd.get("hbm_GBs"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": kd.get("hbm_frac"), "traffic": kd.get("traffic_bytes_per_launch"),
-                    "measure": "L2->fabric bytes (FETCH_SIZE x 2 + WRITE_SIZE, includes Infinity-Cache hits) / "
+                    "measure": f"L2->fabric bytes (FETCH_SIZE x {FETCH_FACTOR.get(dom, 2.0):g}, calibrated in "
+                               f"{FETCH_CALIBRATION}, + WRITE_SIZE; includes Infinity-Cache hits) / "
                                "HIP-event launch time, both from single-stream renders of this workload "
                                "(RT_OPT_STREAMS=1: the timed twin-stream steps overlap two halves' kernels)",
                     "kernel": f"k_{dom}", "kernel_ms_avg": kd["ms_avg"], "launches_per_step": kd["launches"],

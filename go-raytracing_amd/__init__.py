@@ -556,8 +556,8 @@ class Context:
         self.set_option(RT_OPT_TAIL, paths)
 
     def set_overlap(self, mode: int = 0):
-        """RT_OPT_OVERLAP for the next renders: 0 automatic (on in scenes with
-        lights), 1 off, 2 on.  Bounce b's shadow rays and NEE adds run beside
+        """RT_OPT_OVERLAP for the next renders: 0 automatic (off), 1 off, 2 on
+        (scenes with lights).  Bounce b's shadow rays and NEE adds run beside
         bounce b + 1's closest-hit kernel on a second stream per part.  Never
         changes the image."""
         self.set_option(RT_OPT_OVERLAP, mode)

@@ -333,13 +333,16 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   const int auto_twins = ctx->dscene.shade_kind == SHADE_VOL ? 1
                          : tile_px * uint64_t(std::max(1, p->samples_per_pixel)) > kThreeTwinSamples ? 3 : kDefaultTwins;
   // Bounce overlap (run_batches) for scenes with lights: a second stream per
-  // twin.  RTGPU_OVERLAP (tuning knob) / RT_OPT_OVERLAP: 1 off, 2 on.
+  // twin.  RTGPU_OVERLAP (tuning knob) / RT_OPT_OVERLAP: 1 off, 2 on; off by
+  // default: measured slower on C4 at every twin count (DESIGN §3 "Bounce
+  // overlap": the full frame 2150 -> 2046 / 2025 Msamples/s on one / two
+  // twins, 8-way shard sums 218.8 -> 223.7 / 230.7 ms).
   static const int env_overlap = [] {
     const char* e = getenv("RTGPU_OVERLAP");
     return e ? atoi(e) : 0;
   }();
   const int ovl_opt = ctx->opt_overlap ? ctx->opt_overlap : env_overlap;
-  const bool overlap = ctx->dscene.num_lights > 0 && ovl_opt != 1;
+  const bool overlap = ctx->dscene.num_lights > 0 && ovl_opt == 2;
   const int auto_twins2 = overlap ? std::min(auto_twins, kOverlapTwins) : auto_twins;
   const int want_twins = ctx->opt_streams ? ctx->opt_streams : env_twins ? env_twins : auto_twins2;
   const int nt = int(std::max<size_t>(1, std::min<size_t>(size_t(want_twins), tiles.size())));
@@ -1059,6 +1062,11 @@ static int upload_one(rt_ctx* ctx, const rt_scene_desc* scene) {
   UP(images, images);
   UP(image_texels, image_texels);
   UP(env_texels, env.texels);
+  {
+    const uint32_t* rgbe = nullptr;
+    if (!h.env_rgbe.empty() && (rc = upload_vec(ctx, h.env_rgbe, &rgbe))) { free_scene(ctx); return rc; }
+    d.env.rgbe = rgbe;
+  }
   UP(env_pdf, env.pdf);
   UP(env_marginal, env.marginal);
   UP(env_conditional, env.conditional);

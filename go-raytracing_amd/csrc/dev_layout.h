@@ -358,6 +358,8 @@ struct DEnv {
   float rotation;
   float total_power;
   const float* texels;       // width*height*4 (rgb + pad)
+  const uint32_t* rgbe;      // width*height RGBE words (m_r | m_g << 8 | m_b << 16 | e << 24), or nullptr: every
+                             // texel is (m + 0.5) 2^(e - 136) (image_loader.go:364-383), decoded exactly in fp32
   const float* pdf;          // width*height (normalised, hdri.go:217-219)
   const float* marginal;     // height+1
   const float* conditional;  // height*(width+1)

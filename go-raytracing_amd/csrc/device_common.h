@@ -1556,10 +1556,27 @@ __device__ __forceinline__ float pow5(float x) { float x2 = x * x; return (x2 * 
 // ----------------------------------------------------------------------------
 // HDRI (hdri.go)
 // ----------------------------------------------------------------------------
+// An RGBE texel (DEnv::rgbe): (m + 0.5) 2^(e - 136), black for e = 0
+// (rgbeToColor image_loader.go:364-383).  m + 0.5 is exact and ldexpf scales
+// exactly (the result is representable, subnormals included), so the value is
+// the fp32 texel's, bit for bit.
+__device__ __forceinline__ V3 rgbe_texel(uint32_t w) {
+  const int ex = int(w >> 24);
+  if (ex == 0) return mk(0.0f, 0.0f, 0.0f);
+  const int k = ex - 136;
+  return mk(ldexpf(float(w & 0xFFu) + 0.5f, k), ldexpf(float((w >> 8) & 0xFFu) + 0.5f, k),
+            ldexpf(float((w >> 16) & 0xFFu) + 0.5f, k));
+}
 __device__ __forceinline__ V3 texel(const DEnv& e, int x, int y) {
+  if (e.rgbe) return rgbe_texel(e.rgbe[y * e.width + x]);
   const float4 v = reinterpret_cast<const float4*>(e.texels)[y * e.width + x];
   return mk(v.x, v.y, v.z);
 }
+#ifdef RTG_HOST_EMU
+struct rtg_u2u { uint32_t x, y; };
+#else
+typedef uint32_t rtg_u2u __attribute__((ext_vector_type(2), aligned(4)));   // 8 B at 4-B alignment
+#endif
 __device__ __forceinline__ int iclamp(int x, int lo, int hi) {   // image_loader.go:112-120
   if (x < lo) return lo;
   if (x < hi) return x;
@@ -1594,7 +1611,26 @@ __device__ V3 env_sample(const DEnv& e, V3 dir) {          // hdri.go:120-128 + 
   x1 = wrapx(x1);
   y0 = iclamp(y0, 0, e.height);
   y1 = iclamp(y1, 0, e.height);
-  V3 c00 = texel(e, x0, y0), c10 = texel(e, x1, y0), c01 = texel(e, x0, y1), c11 = texel(e, x1, y1);
+  V3 c00, c10, c01, c11;
+  if (e.rgbe) {
+    // RGBE words: a row's two texels are one 8-B load unless x wraps
+    auto row_pair = [&](int y, V3& a, V3& b) {
+      const uint32_t* row = e.rgbe + size_t(y) * size_t(e.width);
+      uint32_t wa, wb;
+      if (x1 == x0 + 1) {
+        const rtg_u2u v = *reinterpret_cast<const rtg_u2u*>(row + x0);
+        wa = v.x; wb = v.y;
+      } else {
+        wa = row[x0]; wb = row[x1];
+      }
+      a = rgbe_texel(wa);
+      b = rgbe_texel(wb);
+    };
+    row_pair(y0, c00, c10);
+    row_pair(y1, c01, c11);
+  } else {
+    c00 = texel(e, x0, y0); c10 = texel(e, x1, y0); c01 = texel(e, x0, y1); c11 = texel(e, x1, y1);
+  }
   V3 c0 = add(scale(c00, 1.0f - fx), scale(c10, fx));
   V3 c1 = add(scale(c01, 1.0f - fx), scale(c11, fx));
   return add(scale(c0, 1.0f - fy), scale(c1, fy));

@@ -1052,6 +1052,36 @@ struct Flattener {
   }
 
   // HDRIEnvironment.BuildDistribution (hdri.go:145-224), fp64, then fp32 tables.
+  // c = (m + 0.5) 2^(e - 136) for all three components (one e), or all zero
+  // (e = 0: black); true when the word decodes back to c bit for bit the way
+  // the device does (ldexpf of m + 0.5, device_common.h rgbe_texel)
+  static bool rgbe_encode(const float* c, uint32_t& word) {
+    if (c[0] == 0.0f && c[1] == 0.0f && c[2] == 0.0f && !std::signbit(c[0]) && !std::signbit(c[1]) && !std::signbit(c[2])) {
+      word = 0u;
+      return true;
+    }
+    int q = 0;
+    uint32_t m[3];
+    for (int k = 0; k < 3; ++k) {
+      if (!(c[k] > 0.0f) || !std::isfinite(c[k])) return false;
+      int ex = 0;
+      const double f = std::frexp(double(c[k]), &ex);
+      int64_t odd = int64_t(std::ldexp(f, 53));   // c = odd 2^(ex - 53), made odd below
+      int qk = ex - 53;
+      while ((odd & 1) == 0) { odd >>= 1; ++qk; }
+      if (odd > 511) return false;
+      if (k > 0 && qk != q) return false;
+      q = qk;
+      m[k] = uint32_t((odd - 1) / 2);
+    }
+    const int e = q + 1 + 136;
+    if (e < 1 || e > 255) return false;
+    word = m[0] | (m[1] << 8) | (m[2] << 16) | (uint32_t(e) << 24);
+    for (int k = 0; k < 3; ++k)
+      if (std::ldexp(float(m[k]) + 0.5f, e - 136) != c[k]) return false;
+    return true;
+  }
+
   void environment() {
     const rt_environment* e = d->environment;
     if (!e) return;
@@ -1065,6 +1095,15 @@ struct Flattener {
     S.env_texels.assign(size_t(W) * H * 4, 0.f);
     for (size_t i = 0; i < size_t(W) * H; ++i)
       for (int c = 0; c < 3; ++c) S.env_texels[i * 4 + c] = float(e->rgb[i * 3 + c]);
+    // The RGBE form (4 B per texel instead of 16): an HDR file's texels are
+    // (m + 0.5) 2^(e - 136) with one exponent per texel (rgbeToColor
+    // image_loader.go:364-383), exact in fp32 over the whole exponent range
+    // (at most 9 significant bits, the smallest 2^-136).  Used only when
+    // every texel re-encodes and decodes back to its fp32 value bit for bit
+    // (rgbe_encode), so the device's bilinear inputs are unchanged.
+    S.env_rgbe.assign(size_t(W) * H, 0u);
+    for (size_t i = 0; i < size_t(W) * H; ++i)
+      if (!rgbe_encode(&S.env_texels[i * 4], S.env_rgbe[i])) { S.env_rgbe.clear(); break; }
     if (!S.env_use_is) return;
     std::vector<double> pdf(size_t(W) * H), rows(H, 0.0), marg(H + 1), cond(size_t(H) * (W + 1));
     double total = 0.0;

@@ -48,6 +48,7 @@ struct HostScene {
   int env_valid = 0, env_w = 0, env_h = 0, env_use_is = 0;
   float env_rotation = 0.f, env_total_power = 0.f;
   std::vector<float> env_texels, env_pdf, env_marginal, env_conditional;
+  std::vector<uint32_t> env_rgbe;    // the texels as RGBE words when every one is exactly one (else empty)
   int stack_needed = 0;
   int tlas_depth = 0, blas_depth = 0;   // BVH2 levels
   int tlas_need4 = 0, blas_need4 = 0;   // BVH4 stack entries along the worst root-to-leaf path

@@ -370,8 +370,9 @@ int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t ma
  *     only input being bounce b's scattered rays (the reference's worker
  *     carries one sample through every bounce, bucket_renderer.go:257-301,
  *     camera.go:443-518).  Same operations per path in the same order: the
- *     frame is bit-identical.  0 (default) = automatic (on, at most two
- *     parts), 1 = off, 2 = on.                                           */
+ *     frame is bit-identical.  0 (default) = automatic (off: measured
+ *     slower on CornellBoxLucy), 1 = off, 2 = on (at most two
+ *     parts unless RT_OPT_STREAMS says otherwise).                       */
 enum { RT_OPT_BLAS_BUILDER = 1, RT_OPT_TLAS_BUILDER = 2, RT_OPT_NODE_FORMAT = 3,
        RT_OPT_BATCH_SLOTS = 4, RT_OPT_REFILL = 5, RT_OPT_MAX_BLOCKS = 6, RT_OPT_STREAMS = 7,
        RT_OPT_VOLUMES = 8, RT_OPT_BVH4_COLLAPSE = 9, RT_OPT_DEALING = 10, RT_OPT_DEAL_FIRST = 11,

@@ -92,7 +92,7 @@ static int load(const char* name, int width, const char* asset_dir, EmuScene& E)
   d.tlas = h.tlas;
   d.env.valid = h.env_valid; d.env.width = h.env_w; d.env.height = h.env_h; d.env.use_is = h.env_use_is;
   d.env.rotation = h.env_rotation; d.env.total_power = h.env_total_power;
-  d.env.texels = ptr(h.env_texels); d.env.pdf = ptr(h.env_pdf); d.env.marginal = ptr(h.env_marginal);
+  d.env.texels = ptr(h.env_texels); d.env.rgbe = h.env_rgbe.empty() ? nullptr : h.env_rgbe.data(); d.env.pdf = ptr(h.env_pdf); d.env.marginal = ptr(h.env_marginal);
   d.env.conditional = ptr(h.env_conditional);
   d.num_planes = int(h.planes.size()); d.num_lights = int(h.lights.size());
   d.num_materials = int(h.materials.size()); d.num_textures = int(h.textures.size());

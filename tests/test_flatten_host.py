@@ -86,6 +86,8 @@ def test_wavefront_kernels_under_asan_match_oracle(wave, O, g, tmp_path, name, b
         args.append(str(batch))   # one sample per batch: several batches
     r = subprocess.run(args, capture_output=True, text=True, env=_env(), timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    if name in ("hdri-test", "hdri-nee"):   # the HDR asset's texels in their 4-B RGBE form (DEnv::rgbe)
+        assert json.loads(r.stdout.strip().splitlines()[-1])["rgbe"] == 1
     kw = dict(width=width)
     if name == "cornell-lucy":
         kw.update(lucy_rings=60, lucy_cols=80)

@@ -235,3 +235,41 @@ def test_tail_kernel_same_frame(g, name, kw, nodes):
             assert np.array_equal(f, ref), k
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("name,kw,nodes,spp", [("cornell-lucy", dict(width=320, aspect=16.0 / 9.0), "fp32", 8),
+                                               ("cornell", dict(width=96), "fp32", 16),
+                                               ("hdri-nee", dict(width=96), "fp32", 8),
+                                               ("cornell-smoke", dict(width=96), "quant8", 8),
+                                               ("cornell-lucy", dict(width=160, aspect=16.0 / 9.0), "wide8", 8)])
+def test_bounce_overlap_same_frame(g, name, kw, nodes, spp):
+    """RT_OPT_OVERLAP: bounce b's k_shadow / k_nee_apply on a second stream
+    per part beside bounce b + 1's k_extend (parity sets of the NEE counters,
+    a spill area per stream) renders the same frame, bit for bit, as the
+    serial schedule, with one to three parts and several batches per frame
+    (the host emulation runs the most separated order under ASan,
+    tests/test_flatten_host.py::test_bounce_overlap_bit_identical).  Values
+    outside 0..2 are refused."""
+    s = g.Scene(name, **kw)
+    cam = s.camera
+    p = g.make_params(spp, cam.max_depth, seed=13)
+    c = g.Context(0)
+    try:
+        for bad in (-1, 3):
+            with pytest.raises(g.RTError):
+                c.set_option(g.RT_OPT_OVERLAP, bad)
+        c.set_node_format(nodes)
+        c.upload(s.desc)
+        frames = {}
+        for overlap in (1, 2):
+            for streams in (1, 2, 3):
+                for slots in (0, 3 * cam.image_width * cam.image_height):   # one batch / several batches
+                    c.set_overlap(overlap)
+                    c.set_schedule(streams=streams, batch_slots=slots)
+                    frames[overlap, streams, slots], _ = c.render(cam, p)
+        ref = frames[1, 1, 0]
+        assert np.isfinite(ref).all() and ref.sum() > 0
+        for k, f in frames.items():
+            assert np.array_equal(f, ref), k
+    finally:
+        c.close()

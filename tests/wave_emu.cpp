@@ -154,7 +154,7 @@ int main(int argc, char** argv) {
   if (!f) return 5;
   fwrite(out.data(), sizeof(float), out.size(), f);
   fclose(f);
-  printf("{\"width\": %d, \"height\": %d, \"slots\": %zu, \"overflow\": %d, \"wide\": %d, \"nodes8\": %zu}\n", cam.width,
-         cam.height, S, err, d.wide_nodes, E.h.nodes8.size());
+  printf("{\"width\": %d, \"height\": %d, \"slots\": %zu, \"overflow\": %d, \"wide\": %d, \"nodes8\": %zu, \"rgbe\": %d}\n",
+         cam.width, cam.height, S, err, d.wide_nodes, E.h.nodes8.size(), d.env.rgbe != nullptr ? 1 : 0);
   return err ? 6 : 0;
 }
