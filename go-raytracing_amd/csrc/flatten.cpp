@@ -748,6 +748,9 @@ struct Flattener {
     return false;
   }
 
+  std::vector<uint8_t> nocut;   // BVH2 nodes that stay BVH4 node roots (RotateX / RotateZ children, tlas_item)
+  bool is_nocut(uint32_t n2) const { return n2 < nocut.size() && nocut[n2] != 0; }
+
   uint32_t tlas_item(int g, int depth, Box& box) {
     if (depth > 200) { fail(RT_ERR_UNSUPPORTED, "world BVH too deep"); return empty_leaf; }
     if (depth > S.tlas_depth) S.tlas_depth = depth;
@@ -770,11 +773,26 @@ struct Flattener {
       // BVHNode.Hit (bvh.go:219-239) tests only its own bbox, never a
       // child's: a child that is not a BVH node is reached whenever this
       // node is.  A slot box only matters where the child's Hit can report
-      // hits outside its bbox (a RotateX / RotateZ below it): such a slot
-      // gets this node's box, which the reference did test
+      // hits outside its bbox (a RotateX / RotateZ below it).  Such a slot
+      // gets an unbounded box (never culled), and this node stays a BVH4
+      // node of its own (nocut): its box is then tested as a slot of its
+      // parent, at the moment the reference tests it (popped in DFS order,
+      // against the closest hit then), while its children are visited in
+      // order with no box test, the right one over [tmin, closest hit of the
+      // left] (the parent's box given to such a slot was tested
+      // again after the left sibling's hit and could drop the right one's
+      // closer hit outside that box)
       DNode& n = S.nodes[idx];
-      store_box(n.l, H(h.a).kind != RT_BVH_NODE && under_rot_xz(h.a, 0) ? box : lb);
-      store_box(n.r, H(h.b).kind != RT_BVH_NODE && under_rot_xz(h.b, 0) ? box : rb);
+      const bool rot_l = H(h.a).kind != RT_BVH_NODE && under_rot_xz(h.a, 0);
+      const bool rot_r = H(h.b).kind != RT_BVH_NODE && under_rot_xz(h.b, 0);
+      Box unbounded;
+      for (int a = 0; a < 3; ++a) { unbounded.b[2 * a] = -kInf; unbounded.b[2 * a + 1] = kInf; }
+      store_box(n.l, rot_l && !lb.empty() ? unbounded : lb);
+      store_box(n.r, rot_r && !rb.empty() ? unbounded : rb);
+      if (rot_l || rot_r) {
+        if (nocut.size() <= size_t(idx)) nocut.resize(size_t(idx) + 1, 0);
+        nocut[size_t(idx)] = 1;
+      }
       n.litem = lb.empty() ? empty_leaf : li;
       n.ritem = rb.empty() ? empty_leaf : ri;
       return (ITEM_NODE << ITEM_SHIFT) | uint32_t(idx);
@@ -1199,6 +1217,8 @@ struct Flattener {
       if (c[k] < c[kb]) kb = k;
     c[1] = half_area(box) + c[kb];
     s[1] = int8_t(kb);
+    if (is_nocut(n2))   // never cut through: only ever one child item of its parent
+      for (int k = 2; k <= 4; ++k) c[k] = std::numeric_limits<double>::infinity();
     dp_cost[n2] = c;
     dp_split[n2] = s;
     dp_done[n2] = 1;
@@ -1237,7 +1257,7 @@ struct Flattener {
       int best = -1;
       double ba = -1.0;
       for (int c = 0; c < nc; ++c)
-        if ((ch[c].item >> ITEM_SHIFT) == ITEM_NODE) {
+        if ((ch[c].item >> ITEM_SHIFT) == ITEM_NODE && !is_nocut(ch[c].item & ITEM_MASK)) {
           const double a = half_area(ch[c].box);
           if (a > ba) { ba = a; best = c; }
         }
