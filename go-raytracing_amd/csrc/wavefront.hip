@@ -85,21 +85,11 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
   return uint32_t(__popcll(m & ((1ull << __lane_id()) - 1ull)));
 }
 
+// counter block words: samples, then the Cnt fields in declaration order
 __device__ __forceinline__ void add_counters(unsigned long long* c, const Cnt& n, uint32_t samples) {
-  atomicAdd(c + 0, (unsigned long long)samples);
-  atomicAdd(c + 1, (unsigned long long)n.rays);
-  atomicAdd(c + 2, (unsigned long long)n.shadow);
-  atomicAdd(c + 3, (unsigned long long)n.nodes);
-  atomicAdd(c + 4, (unsigned long long)n.sph);
-  atomicAdd(c + 5, (unsigned long long)n.quad);
-  atomicAdd(c + 6, (unsigned long long)n.tri);
-  atomicAdd(c + 7, (unsigned long long)n.plane);
-  atomicAdd(c + 8, (unsigned long long)n.inst);
-  atomicAdd(c + 9, (unsigned long long)n.vol);
-  atomicAdd(c + 10, (unsigned long long)n.mat);
-  atomicAdd(c + 11, (unsigned long long)n.env);
-  atomicAdd(c + 12, (unsigned long long)n.ibox);
-  atomicAdd(c + 13, (unsigned long long)n.spill);
+  const uint32_t f[13] = {n.rays, n.shadow, n.nodes, n.sph, n.quad, n.tri, n.plane, n.inst, n.vol, n.mat, n.env, n.ibox, n.spill};
+  atomicAdd(c, (unsigned long long)samples);
+  for (int k = 0; k < 13; ++k) atomicAdd(c + 1 + k, (unsigned long long)f[k]);
 }
 
 // ---------------------------------------------------------------- camera
@@ -543,6 +533,20 @@ __host__ __device__ inline size_t shade_lds_bytes(const DScene& sc) {
                                     size_t(sc.num_lights) * sizeof(DLight)
                               : 0;
 }
+// Copy the block's material / texture / light tables into its dynamic LDS
+// (every thread of the block) and point the scene at them.
+__device__ __forceinline__ void shade_tables_to_lds(DScene& sc, char* s_dyn) {
+  DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
+  DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
+  DLight* const s_light = reinterpret_cast<DLight*>(s_tex + sc.num_textures);
+  for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = sc.materials[i];
+  for (int i = threadIdx.x; i < sc.num_textures; i += blockDim.x) s_tex[i] = sc.textures[i];
+  for (int i = threadIdx.x; i < sc.num_lights; i += blockDim.x) s_light[i] = sc.lights[i];
+  __syncthreads();
+  sc.materials = s_mat;
+  sc.textures = s_tex;
+  sc.lights = s_light;
+}
 
 // k_shade occupancy per variant (waves per SIMD):
 //   full (Noise / Image textures): 4 (128 VGPRs; 5 and 6 waves spill 38 and
@@ -588,18 +592,7 @@ static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScen
   // table read is a ds_read.  Chosen at run time, they were generic pointers
   // and every material / texture / light read a flat load.
   constexpr bool kLdsTables = kShade != SHADE_FULL;
-  if (kLdsTables || shade_tables_fit(sc)) {
-    DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
-    DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
-    DLight* const s_light = reinterpret_cast<DLight*>(s_tex + sc.num_textures);
-    for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = scg.materials[i];
-    for (int i = threadIdx.x; i < sc.num_textures; i += blockDim.x) s_tex[i] = scg.textures[i];
-    for (int i = threadIdx.x; i < sc.num_lights; i += blockDim.x) s_light[i] = scg.lights[i];
-    __syncthreads();
-    sc.materials = s_mat;
-    sc.textures = s_tex;
-    sc.lights = s_light;
-  }
+  if (kLdsTables || shade_tables_fit(sc)) shade_tables_to_lds(sc, s_dyn);
   const uint32_t n = *count;
   const uint32_t gs = gridDim.x * blockDim.x;
   // reset the next extend's claim counters here: this bounce's k_extend has
@@ -712,18 +705,7 @@ static __global__ __launch_bounds__(256, kTailWaves) void k_tail(DScene scg, DCa
 #endif
   DScene sc = scg;
   lds_nodes_fill<kLds>(sc, lds_nodes);
-  if (kShade != SHADE_FULL || shade_tables_fit(sc)) {   // k_shade's LDS tables
-    DMaterial* const s_mat = reinterpret_cast<DMaterial*>(s_dyn);
-    DTexture* const s_tex = reinterpret_cast<DTexture*>(s_mat + sc.num_materials);
-    DLight* const s_light = reinterpret_cast<DLight*>(s_tex + sc.num_textures);
-    for (int i = threadIdx.x; i < sc.num_materials; i += blockDim.x) s_mat[i] = scg.materials[i];
-    for (int i = threadIdx.x; i < sc.num_textures; i += blockDim.x) s_tex[i] = scg.textures[i];
-    for (int i = threadIdx.x; i < sc.num_lights; i += blockDim.x) s_light[i] = scg.lights[i];
-    __syncthreads();
-    sc.materials = s_mat;
-    sc.textures = s_tex;
-    sc.lights = s_light;
-  }
+  if (kShade != SHADE_FULL || shade_tables_fit(sc)) shade_tables_to_lds(sc, s_dyn);   // k_shade's LDS tables
   const uint32_t n = *count;
   const uint32_t nwaves = gridDim.x * ((blockDim.x + 63u) / 64u);
 #ifdef RTG_GUARD

@@ -5,9 +5,10 @@ Writes profiles/pmc_<scene>_<W>x<H>.json:
   hbm_bytes_per_launch, dispatches}
 FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters).  Per
 MI355X_MICROARCH.md (HBM section) FETCH_SIZE counts 64 B per 128-B request
-on gfx950 for wide streaming reads, so it is doubled; the traversal's
-64-B node / primitive reads are a different access width, so the doubled
-figure is an upper estimate there (stated in DESIGN.md).
+on gfx950 for wide streaming reads, so it is doubled; the same factor holds
+for the traversal's scattered 16-B rows and node steps (one whole-line
+request per missed line: tools/fetch_calib.sh, profiles/r06_fetch_calib.json,
+bench.py FETCH_FACTOR).
 Also copies the kernel-trace stats CSV to profiles/<tag>_kernel_stats.csv.
 """
 import csv
