@@ -17,4 +17,5 @@ for line in open(path):
         rows[cur][m.group(1)] = int(m.group(2))
 for k, v in rows.items():
     if re.search(r"k_(extend|shadow|shade)ILi8ELb0ELb0ELb[01]E|k_shadeILb[01]ELb0ELb0ELb[01]E", k):
-        print(f"{k[7:40]:34s} vgpr {v.get('VGPRs')} vspill {v.get('VGPRs Spill')} sspill {v.get('SGPRs Spill')} occ {v.get('Occupancy [waves/SIMD]')} scratch {v.get('ScratchSize [bytes/lane]')}")
+        name = k.replace("_ZN3rtgL", "_ZN3rtg")   # (kernels with internal linkage since round 6)
+        print(f"{name[7:40]:34s} vgpr {v.get('VGPRs')} vspill {v.get('VGPRs Spill')} sspill {v.get('SGPRs Spill')} occ {v.get('Occupancy [waves/SIMD]')} scratch {v.get('ScratchSize [bytes/lane]')}")
