@@ -570,7 +570,7 @@ constexpr int kShadeFullWaves = 4, kShadeLeanWaves = 7, kShadeMatWaves = 7, kSha
 template <bool kCount, bool kEnvIS, int kShade, bool kFirst>
 static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScene scg, DCamera cam, WaveArgs a, PathStream cs,
                                                const uint32_t* count, PathStream ns, uint32_t* ncount,
-                                               uint32_t* jcount, uint32_t sample_base) {
+                                               uint32_t* jcount, uint32_t sample_base, uint32_t launch_bounce) {
   // Small scene tables (materials, textures, lights) are read from LDS: they
   // sit on every path's dependent-load chain (hit -> material -> texture,
   // light -> light material -> texture).
@@ -640,7 +640,14 @@ static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScen
         slot = asu(o4.w);
         const uint32_t st = asu(b4.w);
         dleft = int(st & 0xFFFFu);
-        bounce = (st >> 16) & 0x7FFFu;
+        // every path of this launch's stream is at the bounce the host names
+        // (k_shade b - 1 wrote them with b): a kernel argument, so the
+        // counter-RNG's inner hash of (bounce, domain, index), uniform over
+        // the wave, runs on the scalar unit (rnd, ctr)
+        bounce = launch_bounce;
+#ifdef RTG_GUARD
+        if (((st >> 16) & 0x7FFFu) != launch_bounce) rtg_guard_note(52, (st >> 16) & 0x7FFFu, launch_bounce);
+#endif
         allow = (st >> 31) != 0u;
         ro = mk(o4.x, o4.y, o4.z);
         rd = mk(d4.x, d4.y, d4.z);
@@ -1061,10 +1068,10 @@ static hipError_t run_batches(const DScene& sc, const DCamera& cam, const WaveAr
         if ((e = mark_begin(plan, uint8_t(KC_SHADE | (t << KC_TWIN_SHIFT)), st)) != hipSuccess) return e;
         if (b == 0)
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, true>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
-                             cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, sample_base);
+                             cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, sample_base, 0u);
         else
           hipLaunchKernelGGL((k_shade<kCount, kEnvIS, kShade, false>), dim3(gsh[t]), dim3(256), shade_lds, st, sc, cam, a, a.s[c],
-                             cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, sample_base);
+                             cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, sample_base, uint32_t(b));
         if ((e = mark_end(plan, st)) != hipSuccess) return e;
         RTG_LAUNCHED("k_shade", b, st);
         // no lights: k_shade writes no NEE job (sampleLightMIS needs a light,

@@ -58,8 +58,9 @@ void run(const DScene& sc, const DCamera& cam, WaveArgs a, uint32_t spp, uint32_
         k_extend<kRing, false, kVol, false, kQuant, kWide>(sc, cam, a, a.s[c], cnt_stream[c], cnt_stream[nx], cnt_sh, fetch_sh,
                                                            fetch_ext, s0);
       if (pending >= 0) { nee(pending); pending = -1; }
-      if (b == 0) k_shade<false, kEnvIS, kShade, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, s0);
-      else k_shade<false, kEnvIS, kShade, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, s0);
+      if (b == 0) k_shade<false, kEnvIS, kShade, true>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, s0, 0u);
+      else k_shade<false, kEnvIS, kShade, false>(sc, cam, a, a.s[c], cnt_stream[c], a.s[nx], cnt_stream[nx], cnt_sh, s0,
+                                                  uint32_t(b));
       if (ovl) pending = b;
       else nee(b);
       // RTG_EMU_TAIL=b: after bounce b the long-tail kernel carries every
