@@ -656,6 +656,16 @@ def main():
                     "requested_exceeds_peak": bool(req_step_GBs > HBM_PEAK_GBS),
                     "traffic_source": pmc_name if pmc else None, "traffic_stale": pmc_stale,
                     "pipeline_ms_avg": round(float(np.mean(w.kernel_ms)), 3)}
+        # the measured stream-read peak on this box: 10 coalesced
+        # passes over 4 GiB, 16x the Infinity Cache, through the C-ABI's kernel
+        try:
+            pk = w.ctx.measure_read_bandwidth(4 << 30, 10)
+            roofline["peak_measured"] = round(pk, 1)
+            roofline["peak_measured_how"] = "rt_measure_read_bandwidth: coalesced 16-B-per-lane reads, 4 GiB x 10 passes"
+            if roofline["achieved"] is not None and pk > 0:
+                roofline["frac_of_measured"] = round(roofline["achieved"] / pk, 4)
+        except Exception as ex:   # an older library (RTGPU_LIB_DIR A/B builds)
+            print(f"bench: no measured read peak ({ex})", file=sys.stderr)
         if roofline["frac"] is not None and roofline["frac"] > 1.0:   # a counter / timing error, not a result
             roofline["error"] = "HBM-side traffic above the peak: the counters or the launch times are wrong"
             print(f"bench: {roofline['error']}", file=sys.stderr)

@@ -189,6 +189,8 @@ def rtgpu() -> C.CDLL:
         lib.rt_count_work_by_kernel.argtypes = [P, C.POINTER(RtCameraDesc), C.POINTER(RtRenderParams),
                                                 C.POINTER(RtWorkCounts)]
         lib.rt_set_kernel_timing.argtypes = [P, C.c_int]
+        if hasattr(lib, "rt_measure_read_bandwidth"):
+            lib.rt_measure_read_bandwidth.argtypes = [P, C.c_uint64, I32, C.POINTER(C.c_double)]
         lib.rt_ctx_set_option.argtypes = [P, I32, I32]
         lib.rt_last_kernel_times.argtypes = [P, C.POINTER(RtKernelTimes)]
         lib.rt_tonemap_rgba8.argtypes = [P, C.POINTER(C.c_float), I32, I32, I32, C.POINTER(C.c_uint8)]
@@ -561,6 +563,13 @@ class Context:
         bounce b + 1's closest-hit kernel on a second stream per part.  Never
         changes the image."""
         self.set_option(RT_OPT_OVERLAP, mode)
+
+    def measure_read_bandwidth(self, nbytes: int = 4 << 30, reps: int = 10) -> float:
+        """The measured HBM read peak (GB/s): `reps` coalesced passes over a
+        fresh `nbytes` device buffer (rt_measure_read_bandwidth)."""
+        gbs = C.c_double(0.0)
+        self._check(self._lib.rt_measure_read_bandwidth(self._h, C.c_uint64(nbytes), reps, C.byref(gbs)))
+        return float(gbs.value)
 
     def set_kernel_timing(self, enable: bool = True):
         self._check(self._lib.rt_set_kernel_timing(self._h, 1 if enable else 0))

@@ -1317,6 +1317,37 @@ int rt_count_work(rt_ctx* ctx, const rt_camera_desc* cam, const rt_render_params
   return RT_OK;
 }
 
+int rt_measure_read_bandwidth(rt_ctx* ctx, uint64_t bytes, int32_t reps, double* gbs) {
+  if (!ctx || !gbs || reps <= 0 || bytes < (uint64_t(1) << 20)) return RT_ERR_INVALID;
+  *gbs = 0.0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = size_t(bytes / sizeof(float4));
+  void* buf = nullptr;
+  float* sink = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  auto done = [&](int rc) {
+    if (buf) (void)hipFree(buf);
+    if (sink) (void)hipFree(sink);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return rc;
+  };
+  if (hipMalloc(&buf, n * sizeof(float4)) != hipSuccess || hipMalloc(reinterpret_cast<void**>(&sink), sizeof(float)) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    return done(set_err(ctx, RT_ERR_HIP, "rt_measure_read_bandwidth: allocation failed"));
+  hipError_t e = hipMemsetAsync(buf, 0, n * sizeof(float4), ctx->stream);
+  if (e == hipSuccess) e = launch_stream_read(static_cast<const float4*>(buf), n, sink, 1, ctx->stream);   // warm-up
+  if (e == hipSuccess) e = hipEventRecord(e0, ctx->stream);
+  if (e == hipSuccess) e = launch_stream_read(static_cast<const float4*>(buf), n, sink, reps, ctx->stream);
+  if (e == hipSuccess) e = hipEventRecord(e1, ctx->stream);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float ms = 0.0f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  if (e != hipSuccess) return done(hip_fail(ctx, e, "rt_measure_read_bandwidth"));
+  *gbs = ms > 0.0f ? double(n) * sizeof(float4) * reps / (double(ms) * 1e6) : 0.0;
+  return done(RT_OK);
+}
+
 int rt_set_kernel_timing(rt_ctx* ctx, int enable) {
   if (!ctx) return RT_ERR_INVALID;
   ctx->timing = enable != 0;

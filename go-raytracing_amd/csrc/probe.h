@@ -21,6 +21,9 @@ hipError_t launch_path_hits(const DScene& sc, const DCamera& cam, const float4* 
                             const uint32_t* count, const uint32_t* pixels, uint32_t npix, uint32_t seed,
                             uint32_t sample, int bounce, int32_t* top, int32_t* prim, float* t, float* ray,
                             hipStream_t st);
+// The roofline's measured peak: `reps` passes of a coalesced 16-B-per-lane
+// read over `n` float4 (rt_measure_read_bandwidth).
+hipError_t launch_stream_read(const float4* src, size_t n, float* sink, int reps, hipStream_t st);
 hipError_t launch_nee_probe(const uint32_t* sj_info, const uint32_t* sj_vis, const float4* ne_a, const uint32_t* count,
                             const uint32_t* pixels, uint32_t npix, int32_t* nee, hipStream_t st);
 

@@ -199,6 +199,30 @@ hipError_t launch_tonemap_buckets(const float* accum, int width, const int4* buc
   return hipGetLastError();
 }
 
+// Coalesced streaming read (16 B per lane, grid-stride, non-temporal as the
+// path streams): the measured HBM read peak the bench line reports beside the
+// 8 TB/s spec.  The sum is stored only if it equals a value no
+// input produces, so the loads stay and nothing is written.
+__global__ __launch_bounds__(256) void stream_read_kernel(const float4* __restrict__ src, size_t n, float* sink) {
+  float s = 0.0f;
+  const size_t gs = size_t(gridDim.x) * blockDim.x;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += gs) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src + i));
+    s += v.x + v.y + v.z + v.w;
+  }
+  if (s == -1.2345e-38f) sink[0] = s;
+}
+
+hipError_t launch_stream_read(const float4* src, size_t n, float* sink, int reps, hipStream_t st) {
+  int dev = 0, cus = 1;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(stream_read_kernel, dim3(cus * 8), dim3(256), 0, st, src, n, sink);
+  return hipGetLastError();
+}
+
 hipError_t launch_path_fill(uint32_t n, int32_t* top, int32_t* prim, float* t, float* ray, int32_t* nee,
                             hipStream_t st) {
   if (n == 0) return hipSuccess;

@@ -432,6 +432,12 @@ int rt_count_work_by_kernel(rt_ctx* ctx, const rt_camera_desc* cam, const rt_ren
 /* Per-launch kernel timing of subsequent renders (off by default; one HIP
  * event before every extend/shade/shadow launch and after every shadow).   */
 int rt_set_kernel_timing(rt_ctx* ctx, int enable);
+/* The measured HBM read peak for the roofline ("plus a
+ * measured stream-read kernel peak on the box"): `reps` passes of a
+ * coalesced 16-B-per-lane read over a fresh device buffer of `bytes`
+ * (>= 1 MiB; larger than the 256-MB Infinity Cache to measure HBM), timed
+ * with HIP events on the context's stream, in GB/s.  Blocks.              */
+int rt_measure_read_bandwidth(rt_ctx* ctx, uint64_t bytes, int32_t reps, double* gbs);
 int rt_last_kernel_times(rt_ctx* ctx, rt_kernel_times* out);
 
 /* RGBA8 quantisation of an accumulated sum (bucket_renderer.go:276-285):

@@ -273,3 +273,14 @@ def test_bounce_overlap_same_frame(g, name, kw, nodes, spp):
             assert np.array_equal(f, ref), k
     finally:
         c.close()
+
+
+def test_measured_read_bandwidth(g, ctx):
+    """rt_measure_read_bandwidth: the roofline's measured HBM read peak (a
+    coalesced stream over 1 GiB, larger than the Infinity Cache) lies between
+    a quarter of the 8 TB/s spec and the spec; bad arguments are refused."""
+    gbs = ctx.measure_read_bandwidth(1 << 30, 4)
+    print(f"measured stream-read peak {gbs:.0f} GB/s")
+    assert 2000.0 < gbs <= 8000.0
+    with pytest.raises(g.RTError):
+        ctx.measure_read_bandwidth(1024, 4)
