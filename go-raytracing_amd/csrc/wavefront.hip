@@ -42,12 +42,13 @@ constexpr int kTravWaves = 7, kVolWaves = 4;
 // in what the LDS leaves beside the stack ring at 7 waves per SIMD (160 KB
 // per CU, allocated in 512-B granules: at most 45 granules, 23040 B, per
 // block).  k_shadow: 16 words per lane (the world ray's 1/d recomputed on
-// instance exit) + 48 nodes = 22 KB.  k_extend keeps the 1/d in LDS (22
+// instance exit) + its prefetched job's direction row (4 words, below) + 20
+// nodes = 22.5 KB.  k_extend keeps the 1/d in LDS (22
 // words per lane, room for 4 nodes, the top of the world BVH): recomputing it
 // there to make room for 28 nodes cost 4 % of its single-stream time, more
 // than the nodes returned (DESIGN §3 "LDS node cache").  k_tail (4 waves)
 // keeps the 1/d and 64 nodes.
-constexpr int kLdsNodesExt = 4, kLdsNodesSh = 48, kLdsNodesTail = 64;
+constexpr int kLdsNodesExt = 4, kLdsNodesSh = 20, kLdsNodesTail = 64;
 constexpr int lds_nodes_for(int k, bool kQuant, bool kWide) { return (kQuant || kWide) ? 0 : k; }
 constexpr int lds_node_rows(int k) { return k > 0 ? k * 8 : 1; }
 
@@ -788,6 +789,12 @@ static __global__ __launch_bounds__(256, TRAV_WAVES(kVol, kCount)) void k_shadow
   __shared__ uint32_t lds_stack[(STACK + kWorldRayWords) * 256];   // stack ring + world ray
   constexpr int kLds = lds_nodes_for(kLdsNodesSh, kQuant, kWide);
   __shared__ float4 lds_nodes[lds_node_rows(kLds)];
+  // the prefetched job's area-light direction + tmax, per lane: held in LDS,
+  // not in four VGPRs across every traversal step (7 VGPRs spilled at the
+  // 72-register cap with it in registers, 1 without; WRITE_SIZE per launch
+  // 3.99 -> 2.18 GB, the spill scratch; C4 +0.8 %).  Its
+  // LDS took 28 of the 48 cached nodes.
+  __shared__ float4 lds_pf[256];
   lds_nodes_fill<kLds>(sc, lds_nodes);
   // the next bounce's claim counters (the other parity set, cnt_fetch_sh:
   // the k_shadow that used it last ran before this one on this stream).  The
@@ -814,7 +821,7 @@ static __global__ __launch_bounds__(256, TRAV_WAVES(kVol, kCount)) void k_shadow
   V3 P = mk(0.0f, 0.0f, 0.0f);
   float4 da = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   // prefetched job
-  float4 qp = da, qa = da, qh = da;
+  float4 qp = da, qh = da;
   uint32_t qinfo = 1u;
   auto start_ray = [&](int rr, V3 dir, float tmax) -> int {
     if (kCount) cnt.shadow++;
@@ -842,7 +849,7 @@ static __global__ __launch_bounds__(256, TRAV_WAVES(kVol, kCount)) void k_shadow
       P = mk(qp.x, qp.y, qp.z);
       key = asu(qp.w);
       info = qinfo;
-      da = qa;
+      da = lds_pf[threadIdx.x];
       vis = 0u;
       int s;
       if (kEnvIS && (info & 2u)) {
@@ -858,7 +865,7 @@ static __global__ __launch_bounds__(256, TRAV_WAVES(kVol, kCount)) void k_shadow
     if (idx != ITEM_NONE) {
       pn = GIX(claim_perm(idx, n), a.slots, 46);
       qp = ldnt(&a.sj_p[pn]);
-      qa = ldnt(&a.sj_a[pn]);
+      lds_pf[threadIdx.x] = ldnt(&a.sj_a[pn]);
       if (kEnvIS) qh = ldnt(&a.sj_h[pn]);
       if (kEnvIS || kVol) qinfo = ldnt(&a.sj_info[pn]);
     }
