@@ -360,42 +360,56 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   }
   const uint32_t npix = uint32_t(px.size());
   const uint32_t spp = uint32_t(p->samples_per_pixel);
-  // Path slots per batch: as many as fit in half the free HBM, up to 512M
-  // (135 GB at 264 B per slot).  Larger batches amortise every launch's
+  // Path slots per batch: as many as fit in 85 % of the free HBM, up to 2^30
+  // (249 GB at 232 B per slot).  Larger batches amortise every launch's
   // ramp-down tail; measured on CornellBoxLucy (Msamples/s): 8M slots 501,
   // 32M 686, 128M 759, 210M 799, the whole 405M-sample frame in one batch
-  // 833.  Samples are split evenly over the batches.  RTGPU_SLOTS overrides
-  // (tuning knob).
+  // 833; on HDRITestScene 1920x1080 x 2000 spp, 8 batches of 518M slots 9571,
+  // 5 of 829M 9703, 4 of 1037M 9820 (profiles/r06_c5_slots_ab.log).  Samples
+  // are split evenly over the batches.  RTGPU_SLOTS overrides (tuning knob).
+  // When the automatic size does not fit after all (another process, or
+  // another context, took memory since hipMemGetInfo), it halves and retries.
   // Per slot: kSlotF4 float4 arrays (wavefront.h) + job info + visibility words.
   constexpr size_t kSlotBytes = size_t(kSlotF4) * sizeof(float4) + 2 * sizeof(uint32_t);
+  constexpr size_t kMinSlots = size_t(1) << 20;
   static const size_t env_slots = [] {
     const char* e = getenv("RTGPU_SLOTS");
     return e && atol(e) > 0 ? size_t(atol(e)) : size_t(0);
   }();
   size_t target = ctx->opt_slots ? ctx->opt_slots : env_slots;
-  if (!target) {
+  const bool auto_slots = target == 0;
+  if (auto_slots) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = size_t(8) << 30;
     free_b += ctx->wslots * kSlotBytes;   // the current batch buffers can be reused
-    target = std::min<size_t>(size_t(512) << 20, std::max<size_t>(size_t(1) << 20, free_b / 2 / kSlotBytes));
+    target = std::min<size_t>(size_t(1) << 30, std::max<size_t>(kMinSlots, free_b / 100 * 85 / kSlotBytes));
   }
-  const uint32_t max_spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
-  const uint32_t nbatch = (spp + max_spb - 1) / max_spb;
-  const uint32_t spb = (spp + nbatch - 1) / nbatch;
-  const size_t nslots = size_t(spb) * npix;   // over both twins
+  uint32_t spb = 0;
+  size_t nslots = 0, wq_bytes = 0;
   int rc;
-  // Every twin takes kSlotF4 float4 arrays of its S_t slots and, in `wq`, its
-  // CNT_WORDS_Q queue counters plus two job words per slot: room for
-  // kMaxTwins twins' counters whatever `nt` this render uses (S_t sum to
-  // nslots over the twins).
-  const size_t wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
-  if (ctx->wslots < nslots) {
+  for (;;) {
+    const uint32_t max_spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
+    const uint32_t nbatch = (spp + max_spb - 1) / max_spb;
+    spb = (spp + nbatch - 1) / nbatch;
+    nslots = size_t(spb) * npix;   // over both twins
+    // Every twin takes kSlotF4 float4 arrays of its S_t slots and, in `wq`,
+    // its CNT_WORDS_Q queue counters plus two job words per slot: room for
+    // kMaxTwins twins' counters whatever `nt` this render uses (S_t sum to
+    // nslots over the twins).
+    wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
+    if (ctx->wslots >= nslots) break;
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
     ctx->wslots = 0;
-    if ((rc = ensure(ctx, ctx->wstate, nslots * size_t(kSlotF4) * sizeof(float4)))) return rc;
-    if ((rc = ensure(ctx, ctx->wq, wq_bytes))) return rc;
-    ctx->wslots = nslots;
+    rc = ensure(ctx, ctx->wstate, nslots * size_t(kSlotF4) * sizeof(float4));
+    if (!rc) rc = ensure(ctx, ctx->wq, wq_bytes);
+    if (!rc) { ctx->wslots = nslots; break; }
+    if (rc != RT_ERR_OOM || !auto_slots || target <= kMinSlots || spb == 1) return rc;
+    free_buf(ctx->wstate);
+    free_buf(ctx->wq);
+    (void)hipGetLastError();
+    ctx->error.clear();
+    target = std::max(kMinSlots, target / 2);
   }
   if ((rc = ensure(ctx, ctx->wpix, npix * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->wacc, size_t(npix) * 3 * sizeof(double)))) return rc;

@@ -330,8 +330,8 @@ int rt_last_dealing(const rt_ctx* ctx, int32_t* tiles, int32_t* runs, int32_t ma
 /* Schedule options (take effect at the next render; 0 = automatic).  They
  * change how the work is dealt to the GPU, never the image: the closest hit
  * is independent of the traversal schedule.
- *   RT_OPT_BATCH_SLOTS: path slots per batch (default: from half the free
- *     HBM, at most 512M).
+ *   RT_OPT_BATCH_SLOTS: path slots per batch (default: from 85 % of the
+ *     free HBM, at most 2^30, halved until the allocation succeeds).
  *   RT_OPT_REFILL: idle lanes of a wave (1..64) before it claims a new run
  *     of rays (default 16).
  *   RT_OPT_MAX_BLOCKS: cap on the persistent traversal grids (workgroups).
