@@ -284,3 +284,33 @@ def test_measured_read_bandwidth(g, ctx):
     assert 2000.0 < gbs <= 8000.0
     with pytest.raises(g.RTError):
         ctx.measure_read_bandwidth(1024, 4)
+
+
+def test_batch_slots_follow_free_memory(g):
+    """The automatic batch size (85 % of the free HBM, api.cpp rt_render):
+    with all but about 3 GB of the device held by another allocation, a
+    frame whose one-batch size (37.7 M slots, 8.7 GB) does not fit renders in
+    several batches, and the frame is the one rendered in a single batch once
+    the memory is back."""
+    import torch
+    s = g.Scene("cornell", width=96)
+    cam = s.camera
+    p = g.make_params(4096, cam.max_depth, seed=5)
+    c = g.Context(0)
+    try:
+        c.upload(s.desc)
+        free, _ = torch.cuda.mem_get_info(0)
+        hold = torch.empty(max(0, free - (3 << 30)), dtype=torch.uint8, device="cuda:0")
+        try:
+            tight, _ = c.render(cam, p)
+            left, _ = torch.cuda.mem_get_info(0)
+            assert left < (3 << 30)
+        finally:
+            del hold
+            torch.cuda.empty_cache()
+        c.set_schedule(batch_slots=cam.image_width * cam.image_height * 4096)
+        whole, _ = c.render(cam, p)
+        assert np.isfinite(whole).all() and whole.sum() > 0
+        assert np.array_equal(tight, whole)
+    finally:
+        c.close()
