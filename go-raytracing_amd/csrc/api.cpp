@@ -51,7 +51,6 @@ struct rt_ctx {
   bool kev_recorded = false;
   // wavefront state
   DevBuf wstate, wq, wpix, wacc, wspill;
-  size_t wslots = 0;
   uint32_t* probe_pinned = nullptr;
   int num_cus = 0;
   std::vector<uint32_t> pix_host;
@@ -369,9 +368,16 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   // are split evenly over the batches.  RTGPU_SLOTS overrides (tuning knob).
   // When the automatic size does not fit after all (another process, or
   // another context, took memory since hipMemGetInfo), it halves and retries.
-  // Per slot: kSlotF4 float4 arrays (wavefront.h) + job info + visibility words.
-  constexpr size_t kSlotBytes = size_t(kSlotF4) * sizeof(float4) + 2 * sizeof(uint32_t);
+  // Per slot: kSlotF4 float4 arrays (wavefront.h) + job info + visibility
+  // words; kSlotF4Dark arrays and no job words in a scene without lights
+  // (C5: 128 instead of 232 B, three batches of 1.38G slots instead of four).
+  const bool lit = ctx->dscene.num_lights > 0;
+  const size_t slot_f4 = size_t(lit ? kSlotF4 : kSlotF4Dark);
+  const size_t job_words = lit ? 2 : 0;
+  const size_t slot_bytes = slot_f4 * sizeof(float4) + job_words * sizeof(uint32_t);
   constexpr size_t kMinSlots = size_t(1) << 20;
+  // at most 1.5 * 2^30 slots: a twin's slot indices stay below 2^31
+  constexpr size_t kMaxSlots = size_t(3) << 29;
   static const size_t env_slots = [] {
     const char* e = getenv("RTGPU_SLOTS");
     return e && atol(e) > 0 ? size_t(atol(e)) : size_t(0);
@@ -381,29 +387,29 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
   if (auto_slots) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = size_t(8) << 30;
-    free_b += ctx->wslots * kSlotBytes;   // the current batch buffers can be reused
-    target = std::min<size_t>(size_t(1) << 30, std::max<size_t>(kMinSlots, free_b / 100 * 85 / kSlotBytes));
+    free_b += ctx->wstate.bytes + ctx->wq.bytes;   // the current batch buffers can be reused
+    target = std::min<size_t>(kMaxSlots, std::max<size_t>(kMinSlots, free_b / 100 * 85 / slot_bytes));
   }
   uint32_t spb = 0;
-  size_t nslots = 0, wq_bytes = 0;
+  size_t nslots = 0, wq_bytes = 0, f4_bytes = 0;
   int rc;
   for (;;) {
     const uint32_t max_spb = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, target / npix)));
     const uint32_t nbatch = (spp + max_spb - 1) / max_spb;
     spb = (spp + nbatch - 1) / nbatch;
     nslots = size_t(spb) * npix;   // over both twins
-    // Every twin takes kSlotF4 float4 arrays of its S_t slots and, in `wq`,
-    // its CNT_WORDS_Q queue counters plus two job words per slot: room for
-    // kMaxTwins twins' counters whatever `nt` this render uses (S_t sum to
-    // nslots over the twins).
-    wq_bytes = (nslots * 2 + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
-    if (ctx->wslots >= nslots) break;
+    // Every twin takes slot_f4 float4 arrays of its S_t slots and, in `wq`,
+    // its CNT_WORDS_Q queue counters plus its job words: room for kMaxTwins
+    // twins' counters whatever `nt` this render uses (S_t sum to nslots over
+    // the twins).
+    f4_bytes = nslots * slot_f4 * sizeof(float4);
+    wq_bytes = (nslots * job_words + size_t(kMaxTwins) * CNT_WORDS_Q) * sizeof(uint32_t);
+    if (ctx->wstate.p && ctx->wq.p && ctx->wstate.bytes >= f4_bytes && ctx->wq.bytes >= wq_bytes) break;
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
-    ctx->wslots = 0;
-    rc = ensure(ctx, ctx->wstate, nslots * size_t(kSlotF4) * sizeof(float4));
+    rc = ensure(ctx, ctx->wstate, f4_bytes);
     if (!rc) rc = ensure(ctx, ctx->wq, wq_bytes);
-    if (!rc) { ctx->wslots = nslots; break; }
+    if (!rc) break;
     if (rc != RT_ERR_OOM || !auto_slots || target <= kMinSlots || spb == 1) return rc;
     free_buf(ctx->wstate);
     free_buf(ctx->wq);
@@ -454,7 +460,7 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
       HIPCHK(hipEventCreateWithFlags(&ctx->ev_shade[t], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&ctx->ev_nee[t], hipEventDisableTiming));
     }
-  // each twin: kSlotF4 arrays of its own S_t slots, its queue counters and
+  // each twin: slot_f4 arrays of its own S_t slots, its queue counters and
   // job words, its slice of the pixel list and the fp64 sums, its spill area
   WaveArgs as[kMaxTwins]{};
   hipStream_t sts[kMaxTwins] = {st};
@@ -470,13 +476,15 @@ int render_wave(rt_ctx* ctx, const DCamera& dc, const rt_render_params* p, const
       a.s[k] = PathStream{sb, sb + S, sb + 2 * S};
     }
     a.hit = fbase + 6 * S; a.Lout = fbase + 7 * S;
-    a.sj_p = fbase + 8 * S; a.sj_a = fbase + 9 * S; a.sj_h = fbase + 10 * S;
-    a.ne_a = fbase + 11 * S; a.ne_h = fbase + 12 * S; a.ne_beta = fbase + 13 * S;
-    fbase += size_t(kSlotF4) * S;
     a.counts = qbase;
-    a.sj_info = qbase + CNT_WORDS_Q;
-    a.sj_vis = a.sj_info + S;
-    qbase += CNT_WORDS_Q + 2 * S;
+    if (lit) {   // without lights no kernel touches the NEE job arrays
+      a.sj_p = fbase + 8 * S; a.sj_a = fbase + 9 * S; a.sj_h = fbase + 10 * S;
+      a.ne_a = fbase + 11 * S; a.ne_h = fbase + 12 * S; a.ne_beta = fbase + 13 * S;
+      a.sj_info = qbase + CNT_WORDS_Q;
+      a.sj_vis = a.sj_info + S;
+    }
+    fbase += slot_f4 * S;
+    qbase += CNT_WORDS_Q + job_words * S;
     a.pixels = static_cast<const uint32_t*>(ctx->wpix.p) + pix_off;
     a.npix = twin_npix[t];
     a.acc = static_cast<double*>(ctx->wacc.p) + size_t(pix_off) * 3;
@@ -1556,7 +1564,7 @@ int path_probe(rt_ctx* ctx, const rt_camera_desc* cam, uint32_t seed, int32_t sa
       if (what & 1)
         HIPCHK(launch_path_hits(ctx->dscene, dc, a.hit, a.s[c].o, a.s[c].d, a.counts + (c ? CNT_STREAM1 : CNT_STREAM0),
                                 a.pixels, a.npix, seed, uint32_t(sample), bounce, top, prim, t, ray, ctx->stream));
-      if (what & 2)
+      if ((what & 2) && a.sj_info)   // a scene without lights has no job arrays (render_wave)
         HIPCHK(launch_nee_probe(a.sj_info, a.sj_vis, a.ne_a, a.counts + cnt_shadow(c), a.pixels, a.npix, nee, ctx->stream));
     }
   }

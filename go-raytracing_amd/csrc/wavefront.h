@@ -19,8 +19,11 @@ struct PathStream {
 };
 
 // float4 arrays per path slot: two path streams (3 each), hit, Lout, six NEE
-// job fields; plus two uint32 job words (sj_info, sj_vis).
+// job fields; plus two uint32 job words (sj_info, sj_vis).  Scenes without
+// lights write no NEE job (sampleLightMIS needs a light, camera.go:502): their
+// slots hold the first kSlotF4Dark arrays only, and no job words.
 constexpr int kSlotF4 = 14;
+constexpr int kSlotF4Dark = 8;
 
 struct WaveArgs {
   PathStream s[2];  // ping-pong: bounce b reads s[b&1], writes survivors to s[(b&1)^1]
