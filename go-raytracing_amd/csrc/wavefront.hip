@@ -609,8 +609,9 @@ static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScen
   (void)gs;
   __shared__ uint32_t s_chunk[2];   // double-buffered like s_w / s_b
   uint32_t seg = xcc_id(), tried = 0;
+  const uint32_t nchunks = n_up / blockDim.x;
+  if (threadIdx.x == 0) s_chunk[0] = shade_claim(a.counts + CNT_SHADE_SEG, nchunks, seg, tried);
   for (;; par ^= 1u) {
-    if (threadIdx.x == 0) s_chunk[par] = shade_claim(a.counts + CNT_SHADE_SEG, n_up / blockDim.x, seg, tried);
     __syncthreads();
     const uint32_t chunk = s_chunk[par];
     if (chunk == 0xFFFFFFFFu) break;   // block-uniform
@@ -625,6 +626,10 @@ static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScen
       if (kCount) cnt.rays++;                                    // paths shaded
       const uint32_t ii = GIX(i, a.slots, 41);
       const float4 h = ldnt(&a.hit[ii]);
+      // the block's next chunk, claimed beside the hit load and published by
+      // the next iteration's barrier: the claim's round trip no longer holds
+      // every wave of the block there
+      if (threadIdx.x == 0) s_chunk[par ^ 1u] = shade_claim(a.counts + CNT_SHADE_SEG, nchunks, seg, tried);
       V3 ro, rd;
       int dleft;
       bool allow;
@@ -658,6 +663,9 @@ static __global__ __launch_bounds__(256, SHADE_WAVES(kShade)) void k_shade(DScen
                                                  want_shadow, flags, nstate, tmax_a, P, sd, nbeta, ca, ch, da, dh,
                                                  lout_set, cnt);
     }
+    // (thread 0 is live in every chunk of a 256-thread block; the host
+    // emulation's one-thread blocks also reach the chunks past n)
+    if (!live && threadIdx.x == 0) s_chunk[par ^ 1u] = shade_claim(a.counts + CNT_SHADE_SEG, nchunks, seg, tried);
     if (kFirst && live && !lout_set) stnt(&a.Lout[GIX(slot, a.slots, 44)], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     uint32_t jc = 0, js = 0;
     block_reserve2(cont, want_shadow, ncount, jcount, s_w[par], s_b[par], jc, js);
