@@ -299,13 +299,15 @@ __device__ __forceinline__ void block_reserve2(bool c0, bool c1, uint32_t* q0, u
   const int w = int(threadIdx.x >> 6);
   if (__lane_id() == 0) { sw[0][w] = uint32_t(__popcll(m0)); sw[1][w] = uint32_t(__popcll(m1)); }
   __syncthreads();
-  if (threadIdx.x == 0u) {
+  // lanes 0 and 1 take one queue each: the two reservations are one atomic
+  // instruction (two addresses, so not wave-aggregated into a result read
+  // at once), one round trip before the barrier releases the block (the host
+  // emulation's one-thread blocks take both in turn)
+  for (uint32_t q = threadIdx.x; q < 2u; q += blockDim.x) {
     const int nw = int((blockDim.x + 63u) >> 6);
-    for (int q = 0; q < 2; ++q) {
-      uint32_t tot = 0;
-      for (int k = 0; k < nw; ++k) { const uint32_t c = sw[q][k]; sw[q][k] = tot; tot += c; }
-      sb[q] = tot ? atomicAdd(q ? q1 : q0, tot) : 0u;
-    }
+    uint32_t tot = 0;
+    for (int k = 0; k < nw; ++k) { const uint32_t c = sw[q][k]; sw[q][k] = tot; tot += c; }
+    sb[q] = tot ? atomicAdd(q ? q1 : q0, tot) : 0u;
   }
   __syncthreads();
   p0 = sb[0] + sw[0][w] + lanes_below(m0);
