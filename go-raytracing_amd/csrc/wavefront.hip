@@ -559,7 +559,9 @@ __device__ __forceinline__ void shade_tables_to_lds(DScene& sc, char* s_dyn) {
 //     72-VGPR block fits beside the traversal kernels' 72-VGPR waves when the
 //     twin streams overlap them; its LDS tables are sized to the scene);
 //   material (+ Metal / Dielectric / Isotropic: C2, C3, C5): 7 (C2 3473 /
-//     3502 / 3473 / 3632, C5 8548 / 8684 / 8751 / 8973 at 4 / 5 / 6 / 7);
+//     3502 / 3473 / 3632, C5 8548 / 8684 / 8751 / 8973 at 4 / 5 / 6 / 7;
+//     round 6, 7 / 8 waves: C5 9857 / 9101, C2 3910 / 3752, 8 spilling 25
+//     and 38 VGPRs instead of 12 and 29);
 //   volume (+ the lifted volumes' tests: C3): 6 (records read by scalar
 //     loads; 5 / 6 / 7 waves 1886 / 1927 / 1928 at 96 / 80 / 72 VGPRs, 0 /
 //     16 / 53 spilled).
